@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s chunked (device-resident blob -> cut list), BASELINE.json.
+
+Workload (BASELINE.json configs[1]): a 1 GiB synthetic uniform blob (splitmix64,
+seed 1, generated on device) chunked with desync's default min/avg/max =
+16/64/256 KiB; the blob is in HBM when the timed region starts and one step
+produces the complete cut list in HBM (scan + stitch, libdsx.so).
+
+N > 1 (one process per GPU, torch.distributed over RCCL): rank r holds bytes
+[r GiB, (r+1) GiB) of an N GiB blob (+64 B halo, regenerated locally), chunks
+it speculatively (dsx_shard_local), all-gathers the small seam records
+(RCCL), and resolves its final cut list (dsx_shard_resolve) -- weak scaling.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+GiB = 1 << 30
+MIN, AVG, MAX = 16 * 1024, 64 * 1024, 256 * 1024
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+METRIC = "GiB/s chunked (device-resident blob→cut list), 16/64/256KiB, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gib", type=float, default=1.0, help="GiB per GPU")
+    ap.add_argument("--workload", default="uniform", choices=["uniform", "dedup", "zeros"])
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def make_blob(ctx, t, offset, n, workload):
+    from desync_amd import _lib
+    L = _lib.lib()
+    if workload == "uniform":
+        _lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), offset, n, 1), ctx.h)
+    elif workload == "dedup":
+        _lib.check(L.dsx_gen_dedup(ctx.h, ctypes.c_void_p(t.data_ptr()), offset, n, 2, 0.30),
+                   ctx.h)
+    else:
+        t.zero_()
+
+
+def load_traffic(workload, nbytes):
+    """HBM bytes per scan launch from the committed rocprofv3 PMC pass
+    (profiles/traffic_<workload>.json, FETCH_SIZE x2 gfx950 correction)."""
+    path = os.path.join(REPO, "profiles", f"traffic_{workload}.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if int(d.get("bytes", -1)) == int(nbytes):
+            return float(d["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def cpu_baseline(host_blob, threads):
+    """make.go-style split-and-align (C restatement, oracle/) on host cores."""
+    from oracle import oracle as o
+    sample = host_blob
+    n = sample.size
+    # single thread on a 128 MiB prefix
+    pre = sample[:128 << 20]
+    t0 = time.perf_counter()
+    o.chunk_stream(pre, MIN, AVG, MAX)
+    st = time.perf_counter() - t0
+    # threads: repeat the full sample until ~10 s of CPU work
+    reps, t_total, done = 0, 0.0, 0
+    while True:
+        t0 = time.perf_counter()
+        o.chunk_parallel(sample, MIN, AVG, MAX, threads)
+        t_total += time.perf_counter() - t0
+        reps += 1
+        done += n
+        if t_total * threads >= 10.0 or reps >= 20:
+            break
+    return {
+        "value": round(done / t_total / GiB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{reps}x the same {n / GiB:.2f} GiB blob, C restatement of desync's "
+                   f"Chunker.Next loop with make.go split-and-align over {threads} threads "
+                   f"(oracle/dsx_oracle.c, in memory, no chunk IDs); single-thread "
+                   f"{pre.size / st / GiB:.3f} GiB/s on 128 MiB"),
+        "single_thread_gibs": round(pre.size / st / GiB, 3),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    from desync_amd import _lib
+    import desync_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    ctx = _lib.Context(local)
+    n = int(args.gib * GiB)
+    p = desync_amd.Params(MIN, AVG, MAX)
+    L = _lib.lib()
+
+    # ---------------- inputs (outside the timed region) ----------------
+    halo = 64 if rank > 0 else 0
+    blob = torch.empty(n + halo, dtype=torch.uint8, device="cuda")
+    make_blob(ctx, blob, rank * n - halo, n + halo, args.workload)
+    d_ptr = blob.data_ptr() + halo
+    cap = n // MIN + 4
+    out = torch.empty(cap, dtype=torch.int64, device="cuda")
+    seam = _lib.Seam()
+    seam_sz = ctypes.sizeof(_lib.Seam)
+    host_out = np.empty(cap, dtype=np.uint64)
+
+    def step():
+        if world == 1:
+            _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
+                                        ctypes.c_void_p(out.data_ptr()), cap,
+                                        ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
+                       ctx.h)
+            _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
+            return cnt.value
+        total = n * world
+        _lib.check(L.dsx_shard_local(ctx.h, ctypes.c_void_p(d_ptr), halo, rank * n, n, total,
+                                     ctypes.byref(p.c), ctypes.byref(seam)), ctx.h)
+        mine = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(seam), seam_sz)),
+                                dtype=torch.uint8).to("cuda")
+        gathered = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+        allb = b"".join(g.cpu().numpy().tobytes() for g in gathered)
+        arr = (_lib.Seam * world).from_buffer_copy(allb)
+        _lib.check(L.dsx_shard_resolve(ctx.h, arr, world, rank, host_out.ctypes.data, cap,
+                                       ctypes.byref(cnt), 0), ctx.h)
+        return cnt.value
+
+    cnt = ctypes.c_uint64()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    scan_ms = []
+    stitch_ms = []
+    t0 = time.perf_counter()
+    chunks = 0
+    for _ in range(args.steps):
+        chunks = step()
+        if world == 1:
+            st = ctx.stats()
+            scan_ms.append(st.scan_ms)
+            stitch_ms.append(st.stitch_ms)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_per_step = dt / args.steps * 1000.0
+    value = (n * world * args.steps) / dt / GiB
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic ({args.workload}, splitmix64 seed 1, generated on device)",
+            "config": {
+                "workload": (f"{args.gib:g} GiB {args.workload} blob per GPU, desync make "
+                             f"min/avg/max 16/64/256 KiB, device-resident blob -> cut list in HBM"),
+                "bytes_per_gpu": n,
+                "chunks": int(chunks),
+                "parallelism": f"range-shard x{world}" if world > 1 else "single GPU",
+            },
+        }
+        if world == 1 and scan_ms:
+            avg_scan = float(np.mean(scan_ms))
+            achieved = n / (avg_scan / 1e3) / 1e9
+            traffic = load_traffic(args.workload, n)
+            res["roofline"] = {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "dsx::scan_kernel",
+                "kernel_ms": round(avg_scan, 4),
+                "stitch_ms": round(float(np.mean(stitch_ms)), 4),
+            }
+        if world == 1 and not args.no_cpu:
+            host = blob[halo:].cpu().numpy()
+            res["cpu_baseline"] = cpu_baseline(host, args.cpu_threads)
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

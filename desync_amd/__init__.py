@@ -1,0 +1,27 @@
+"""desync_amd -- MI355X-native content-defined chunker (desync drop-in).
+
+The chunking hot path of folbricht/desync (chunker.go Buzhash scan + cut
+chain, make.go split-and-align) runs as hand-written gfx950 HIP kernels in
+libdsx.so behind the C ABI of include/dsx.h.  This package is the host-side
+mirror of the reference's Go API for that path:
+
+    NewChunker / Chunker.Next / Advance / Min / Avg / Max   (chunker.go)
+    IndexFromFile, ChunkingStats                            (make.go)
+    Index, IndexChunk, Index.WriteTo, IndexFromReader       (index.go)
+    Digest (SHA512256 / SHA256), NullChunk                  (digest.go)
+
+There is no CPU fallback: without libdsx.so or a GPU, calls raise.
+"""
+from .chunker import ChunkerWindowSize, Chunker, NewChunker, Params  # noqa: F401
+from .digest import SHA256, SHA512256, NewNullChunk, NullChunk, set_digest  # noqa: F401
+from .errors import Interrupted  # noqa: F401
+from .index import FormatIndex, Index, IndexChunk, IndexFromReader  # noqa: F401
+from .make import ChunkingStats, IndexFromFile, cut_device, cut_device_result, cut_fd, \
+    cut_host  # noqa: F401
+
+__all__ = [
+    "ChunkerWindowSize", "Chunker", "NewChunker", "Params", "SHA256", "SHA512256", "NullChunk",
+    "NewNullChunk", "set_digest", "Interrupted", "FormatIndex", "Index", "IndexChunk",
+    "IndexFromReader", "ChunkingStats", "IndexFromFile", "cut_device", "cut_device_result",
+    "cut_fd", "cut_host",
+]

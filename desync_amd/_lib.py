@@ -1,0 +1,201 @@
+"""ctypes binding of libdsx.so (the C ABI declared in include/dsx.h).
+
+This is the same binding a Go maintainer writes with cgo;
+here it backs the Python mirror of desync's Chunker / IndexFromFile API.  There
+is deliberately no CPU fallback: if the HIP library is missing or no GPU is
+visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdsx.so")
+
+DSX_OUT_HOST = 0
+DSX_OUT_DEVICE = 1
+DSX_NO_SYNC = 2
+DSX_SEAM_MAX_CANDS = 1024
+DSX_SEAM_MAX_CUTS = 1024
+
+# error codes (include/dsx.h)
+DSX_OK = 0
+DSX_E_MIN_TOO_SMALL = -1
+DSX_E_MIN_GT_MAX = -2
+DSX_E_MIN_GT_AVG = -3
+DSX_E_AVG_GT_MAX = -4
+DSX_E_AVG_RANGE = -5
+DSX_E_INVAL = -6
+DSX_E_CAPACITY = -7
+DSX_E_HIP = -8
+DSX_E_NOMEM = -9
+DSX_E_INTERRUPTED = -10
+DSX_E_IO = -11
+DSX_E_STATE = -12
+DSX_E_INTERNAL = -13
+
+# every symbol include/dsx.h declares (tests check the library exports them)
+EXPORTS = (
+    "dsx_params_init", "dsx_strerror", "dsx_abi_version", "dsx_ctx_create", "dsx_ctx_destroy",
+    "dsx_last_error", "dsx_cancel", "dsx_cut_device", "dsx_sync", "dsx_result", "dsx_cut_host",
+    "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
+    "dsx_stream_done", "dsx_stream_chunk_data", "dsx_shard_local", "dsx_shard_resolve",
+    "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_get_stats",
+)
+
+
+class Params(ctypes.Structure):
+    """dsx_params_t (mirrors the Chunker fields of chunker.go:108-131)."""
+
+    _fields_ = [
+        ("min", ctypes.c_uint64), ("avg", ctypes.c_uint64), ("max", ctypes.c_uint64),
+        ("discriminator", ctypes.c_uint32), ("inverse_odd", ctypes.c_uint32),
+        ("qmax", ctypes.c_uint32), ("qbias", ctypes.c_uint32), ("rot", ctypes.c_int32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("chunks", ctypes.c_uint64), ("candidates", ctypes.c_uint64), ("pieces", ctypes.c_uint64),
+        ("repaired_segments", ctypes.c_uint64), ("dense_fallbacks", ctypes.c_uint64),
+        ("scan_ms", ctypes.c_float), ("stitch_ms", ctypes.c_float),
+    ]
+
+
+class Seam(ctypes.Structure):
+    _fields_ = [
+        ("shard_start", ctypes.c_uint64), ("shard_len", ctypes.c_uint64), ("total", ctypes.c_uint64),
+        ("first_cand_beyond", ctypes.c_uint64), ("exit_cut", ctypes.c_uint64),
+        ("window_end", ctypes.c_uint64), ("ncands", ctypes.c_uint32), ("ncuts", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+        ("cands", ctypes.c_uint64 * DSX_SEAM_MAX_CANDS),
+        ("cuts", ctypes.c_uint64 * DSX_SEAM_MAX_CUTS),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _share_torch_hip_runtime():
+    """A process can drive the GPU through ONE HIP runtime.  PyTorch-ROCm ships
+    its own libamdhip64.so (SONAME libamdhip64.so.7, the same as ROCm's); load
+    it before libdsx.so so that libdsx binds to it and device pointers, streams
+    and RCCL from torch interoperate with the library.  Without torch the
+    system ROCm runtime (/opt/rocm/lib, libdsx's RUNPATH) is used."""
+    try:
+        import torch
+    except ImportError:
+        return
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def lib():
+    """Load libdsx.so; raises ImportError if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                "(make -C desync_amd/csrc). desync_amd has no CPU fallback.")
+        _share_torch_hip_runtime()
+        L = ctypes.CDLL(LIB_PATH)
+        u64, u32, i32, vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+        P = ctypes.POINTER
+        sig = {
+            "dsx_params_init": (i32, [u64, u64, u64, P(Params)]),
+            "dsx_strerror": (ctypes.c_char_p, [i32]),
+            "dsx_abi_version": (i32, []),
+            "dsx_ctx_create": (i32, [i32, P(vp)]),
+            "dsx_ctx_destroy": (i32, [vp]),
+            "dsx_last_error": (ctypes.c_char_p, [vp]),
+            "dsx_cancel": (i32, [vp]),
+            "dsx_cut_device": (i32, [vp, vp, u64, P(Params), vp, u64, P(u64), u32]),
+            "dsx_sync": (i32, [vp]),
+            "dsx_result": (i32, [vp, P(u64)]),
+            "dsx_cut_host": (i32, [vp, vp, u64, P(Params), vp, u64, P(u64)]),
+            "dsx_cut_fd": (i32, [vp, i32, u64, u64, P(Params), vp, u64, P(u64)]),
+            "dsx_stream_begin": (i32, [vp, P(Params)]),
+            "dsx_stream_push": (i32, [vp, vp, u64, i32]),
+            "dsx_stream_pop": (i32, [vp, P(u64), P(u64)]),
+            "dsx_stream_advance": (i32, [vp, u64]),
+            "dsx_stream_done": (i32, [vp]),
+            "dsx_stream_chunk_data": (vp, [vp]),
+            "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), P(Seam)]),
+            "dsx_shard_resolve": (i32, [vp, P(Seam), i32, i32, vp, u64, P(u64), u32]),
+            "dsx_selftest_boundary": (i32, [vp, P(Params), i32, u64, u64, P(u64)]),
+            "dsx_gen_uniform": (i32, [vp, vp, u64, u64, u64]),
+            "dsx_gen_dedup": (i32, [vp, vp, u64, u64, u64, ctypes.c_double]),
+            "dsx_get_stats": (i32, [vp, P(Stats)]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+        return L
+
+
+class DsxError(RuntimeError):
+    def __init__(self, code, detail=""):
+        self.code = code
+        msg = lib().dsx_strerror(code).decode()
+        super().__init__(f"{msg}" + (f": {detail}" if detail else ""))
+
+
+def check(rc, ctx=None):
+    if rc < 0:
+        detail = ""
+        if ctx is not None and rc in (DSX_E_HIP, DSX_E_INTERNAL, DSX_E_NOMEM):
+            d = lib().dsx_last_error(ctx)
+            detail = d.decode() if d else ""
+        raise DsxError(rc, detail)
+    return rc
+
+
+class Context:
+    """One dsx_ctx (HIP streams + device scratch) on a GPU; not thread-safe."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        rc = lib().dsx_ctx_create(int(device), ctypes.byref(h))
+        if rc != DSX_OK:
+            why = lib().dsx_last_error(None)
+            raise DsxError(rc, f"cannot create a dsx context on HIP device {device}"
+                           + (f" ({why.decode()})" if why else ""))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().dsx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self):
+        s = Stats()
+        check(lib().dsx_get_stats(self.h, ctypes.byref(s)), self.h)
+        return s
+
+
+_default = {}
+
+
+def default_context(device=0):
+    ctx = _default.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _default[device] = ctx
+    return ctx

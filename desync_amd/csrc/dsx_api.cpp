@@ -1,0 +1,1070 @@
+// dsx_api.cpp -- C ABI (include/dsx.h) and host engine of libdsx.so.
+//
+// The engine splits a blob into pieces, and per piece enqueues on the
+// context's HIP stream: scan (dsx_scan.hip) -> walk -> fixup -> gather
+// (dsx_stitch.hip).  The chain position is carried between pieces in device
+// memory (DevState.carry), so a multi-piece call needs no host round trip
+// until the end.  Reference interfaces replaced are listed in include/dsx.h.
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/dsx.h"
+#include "dsx_common.h"
+#include "dsx_stitch.h"
+
+namespace dsx {
+template <int MODE>
+__global__ void scan_kernel(ScanArgs a);
+__global__ void walk_kernel(StitchArgs a);
+__global__ void fixup_kernel(StitchArgs a);
+__global__ void gather_kernel(StitchArgs a);
+__global__ void gen_uniform_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed);
+__global__ void gen_dedup_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed,
+                                 uint32_t p_thresh);
+__global__ void boundary_selftest_kernel(TestConsts tc, int mode, uint64_t h0, uint64_t n,
+                                         unsigned long long* mismatches);
+__global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
+                                    uint64_t max, uint64_t* out, uint64_t* info);
+}  // namespace dsx
+
+using namespace dsx;
+
+// --------------------------------------------------------------------------
+// small utilities
+// --------------------------------------------------------------------------
+namespace {
+
+constexpr uint64_t kPieceMax = 8ull << 30;       // bytes per scan launch
+constexpr uint64_t kHostChunk = 256ull << 20;    // host-resident pipeline chunk
+constexpr uint64_t kStreamBatch = 16ull << 20;   // streaming: bytes per device batch
+constexpr uint32_t kWalkLdsCap = 12288;          // candidates per walk workgroup
+constexpr uint32_t kDenseS = 480;                // dense path lane bytes (= slot cap)
+constexpr uint64_t kDensePiece = 32ull << 20;    // dense path piece size
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t want) {
+    if (want <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t sz = want < 16 ? 16 : want;
+    hipError_t e = hipMalloc((void**)&p, sz * sizeof(T));
+    if (e == hipSuccess) n = sz;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct dsx_ctx {
+  int device = 0;
+  int ncu = 256;
+  hipStream_t stream = nullptr, copy_stream = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_t2 = nullptr;
+  hipEvent_t copy_done[2] = {nullptr, nullptr}, comp_done[2] = {nullptr, nullptr};
+  std::atomic<int> cancel{0};
+  std::string err;
+  int force_mode = -1;  // DSX_TEST_MODE env override
+
+  DevBuf<uint32_t> lane_cnt, overflow, rep_cnt, rep_from, flag_list;
+  DevBuf<uint16_t> lane_slot;
+  DevBuf<SegInfo> seg_info;
+  DevBuf<uint64_t> stage, rep, out_off, out;
+  DevBuf<DevState> state;
+  DevBuf<uint8_t> dbuf[2];
+  uint8_t* pinned[2] = {nullptr, nullptr};
+  size_t pinned_sz = 0;
+  DevState* h_state = nullptr;  // pinned mirror
+
+  // streaming state (Chunker.Next over an io.Reader)
+  struct Stream {
+    bool active = false, eof = false, done = false;
+    dsx_params_t p{};
+    std::vector<uint8_t> buf;
+    uint64_t buf_pos = 0, scan_pos = 0, origin = 0, cur = 0, skip = 0, carry = 0;
+    std::deque<uint64_t> cuts;
+    const uint8_t* last_chunk = nullptr;
+  } st;
+
+  // multi-GPU shard state
+  uint64_t shard_start = 0, shard_len = 0, shard_min = 0, shard_max = 0;
+  std::vector<uint64_t> shard_cuts;
+
+  dsx_stats_t stats{};
+  // per-piece timing events of the current call: {before scan, after scan, after gather}
+  std::vector<hipEvent_t> pev;
+  uint32_t npiece_call = 0;
+
+  // pending DSX_NO_SYNC call (re-run synchronously on the dense path if needed)
+  struct Pending {
+    bool active = false;
+    const void* d_blob = nullptr;
+    uint64_t len = 0, cap = 0;
+    dsx_params_t p{};
+    uint64_t* out = nullptr;
+  } pend;
+};
+
+// Grow a device buffer; outstanding work may still use the old allocation, so
+// drain both streams before freeing it.  Allocates 25% headroom.
+template <class T>
+static hipError_t grow(dsx_ctx* c, DevBuf<T>& b, size_t n) {
+  if (b.p && b.n >= n) return hipSuccess;
+  if (b.p) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->copy_stream);
+  }
+  return b.ensure(n + n / 4 + 64);
+}
+
+static int set_hip_err(dsx_ctx* c, hipError_t e, const char* what) {
+  char buf[256];
+  snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  c->err = buf;
+  return e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? DSX_E_NOMEM : DSX_E_HIP;
+}
+
+#define HIPCHK(ctx, expr)                                  \
+  do {                                                     \
+    hipError_t e_ = (expr);                                \
+    if (e_ != hipSuccess) return set_hip_err(ctx, e_, #expr); \
+  } while (0)
+
+// --------------------------------------------------------------------------
+// parameters (chunker.go:13-28, 134-171)
+// --------------------------------------------------------------------------
+static uint32_t discriminator_from_avg(uint64_t avg) {
+  // float64, evaluated without FMA contraction (built with -ffp-contract=off)
+  volatile double a = (double)avg;
+  volatile double den = -1.42888852e-7 * a;
+  den = den + 1.33237515;
+  volatile double q = a / den;
+  if (!(q >= 1.0 && q < 4294967296.0)) return 0u;
+  return (uint32_t)q;
+}
+
+static uint32_t mod_inverse32(uint32_t d) {
+  uint32_t x = d;
+  for (int i = 0; i < 5; ++i) x *= 2u - d * x;
+  return x;
+}
+
+extern "C" int dsx_abi_version(void) { return DSX_ABI_VERSION; }
+
+extern "C" int dsx_params_init(uint64_t min, uint64_t avg, uint64_t max, dsx_params_t* out) {
+  if (!out) return DSX_E_INVAL;
+  if (min < 48) return DSX_E_MIN_TOO_SMALL;
+  if (min > max) return DSX_E_MIN_GT_MAX;
+  if (min > avg) return DSX_E_MIN_GT_AVG;
+  if (avg > max) return DSX_E_AVG_GT_MAX;
+  const uint32_t d = discriminator_from_avg(avg);
+  if (d == 0) return DSX_E_AVG_RANGE;
+  const uint32_t k = (uint32_t)__builtin_ctz(d);
+  const uint32_t odd = d >> k;
+  memset(out, 0, sizeof *out);
+  out->min = min;
+  out->avg = avg;
+  out->max = max;
+  out->discriminator = d;
+  out->inverse_odd = mod_inverse32(odd);
+  out->qbias = odd > 1u ? 1u : 0u;
+  out->qmax = 0xFFFFFFFFu / d - out->qbias;
+  out->rot = (int32_t)k;
+  return DSX_OK;
+}
+
+extern "C" const char* dsx_strerror(int code) {
+  switch (code) {
+    case DSX_OK: return "ok";
+    case DSX_E_MIN_TOO_SMALL: return "min chunk size too small, must be over 48";
+    case DSX_E_MIN_GT_MAX: return "min chunk size must not be greater than max";
+    case DSX_E_MIN_GT_AVG: return "min chunk size must not be greater than avg";
+    case DSX_E_AVG_GT_MAX: return "avg chunk size must not be greater than max";
+    case DSX_E_AVG_RANGE: return "avg chunk size out of range for discriminatorFromAvg";
+    case DSX_E_INVAL: return "invalid argument";
+    case DSX_E_CAPACITY: return "output capacity too small";
+    case DSX_E_HIP: return "HIP runtime error";
+    case DSX_E_NOMEM: return "out of memory";
+    case DSX_E_INTERRUPTED: return "interrupted";
+    case DSX_E_IO: return "I/O error";
+    case DSX_E_STATE: return "invalid stream state";
+    case DSX_E_INTERNAL: return "internal error";
+    default: return "unknown error";
+  }
+}
+
+static TestConsts make_tc(const dsx_params_t* p) {
+  TestConsts tc;
+  tc.d = p->discriminator;
+  tc.dm1 = p->discriminator - 1u;
+  tc.inv = p->inverse_odd;
+  tc.qmax = p->qmax;
+  tc.qbias = p->qbias;
+  tc.rot = (uint32_t)p->rot;
+  tc.rcp = 1.0f / (float)p->discriminator;
+  tc.c0 = (float)(0.5 - (double)(p->discriminator - 1u) / (double)p->discriminator);
+  return tc;
+}
+
+// float-reciprocal test is exact for 2048 < d < 2^24 (DESIGN.md "Boundary test")
+static int pick_mode(const dsx_ctx* c, uint32_t d) {
+  if (c->force_mode == 0 || c->force_mode == 1) return c->force_mode;
+  return (d > 2048u && d < (1u << 24)) ? 1 : 0;
+}
+
+// --------------------------------------------------------------------------
+// context
+// --------------------------------------------------------------------------
+static char g_create_err[256];
+
+extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
+  if (!out) return DSX_E_INVAL;
+  *out = nullptr;
+  g_create_err[0] = 0;
+  dsx_ctx* c = new dsx_ctx();
+  c->device = device;
+#define CREATE_STEP(expr)                                                              \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      snprintf(g_create_err, sizeof g_create_err, "%s: %s (%d)", #expr,                \
+               hipGetErrorString(e_), (int)e_);                                        \
+      dsx_ctx_destroy(c);                                                              \
+      return e_ == hipErrorOutOfMemory ? DSX_E_NOMEM : DSX_E_HIP;                      \
+    }                                                                                  \
+  } while (0)
+  CREATE_STEP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  CREATE_STEP(hipGetDeviceProperties(&prop, device));
+  c->ncu = prop.multiProcessorCount;
+  if (const char* m = getenv("DSX_TEST_MODE")) c->force_mode = atoi(m);
+  CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  CREATE_STEP(hipEventCreate(&c->ev_t0));
+  CREATE_STEP(hipEventCreate(&c->ev_t1));
+  CREATE_STEP(hipEventCreate(&c->ev_t2));
+  for (int i = 0; i < 2; ++i) {
+    CREATE_STEP(hipEventCreateWithFlags(&c->copy_done[i], hipEventDisableTiming));
+    CREATE_STEP(hipEventCreateWithFlags(&c->comp_done[i], hipEventDisableTiming));
+  }
+  CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(DevState)));
+  CREATE_STEP(c->state.ensure(1));
+  CREATE_STEP(c->overflow.ensure(1));
+#undef CREATE_STEP
+  *out = c;
+  return DSX_OK;
+}
+
+extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
+  if (!c) return DSX_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  c->lane_cnt.release(); c->overflow.release(); c->rep_cnt.release(); c->rep_from.release();
+  c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
+  c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
+  c->dbuf[0].release(); c->dbuf[1].release();
+  for (auto& p : c->pinned) if (p) (void)hipHostFree(p);
+  if (c->h_state) (void)hipHostFree(c->h_state);
+  hipEvent_t evs[] = {c->ev_t0, c->ev_t1, c->ev_t2, c->copy_done[0], c->copy_done[1],
+                      c->comp_done[0], c->comp_done[1]};
+  for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  delete c;
+  return DSX_OK;
+}
+
+extern "C" const char* dsx_last_error(dsx_ctx_t* c) { return c ? c->err.c_str() : g_create_err; }
+
+extern "C" int dsx_cancel(dsx_ctx_t* c) {
+  if (!c) return DSX_E_INVAL;
+  c->cancel.store(1);
+  return DSX_OK;
+}
+
+extern "C" int dsx_get_stats(dsx_ctx_t* c, dsx_stats_t* out) {
+  if (!c || !out) return DSX_E_INVAL;
+  *out = c->stats;
+  return DSX_OK;
+}
+
+// --------------------------------------------------------------------------
+// engine
+// --------------------------------------------------------------------------
+struct CallCfg {
+  const dsx_params_t* p;
+  uint64_t L;        // blob length (final piece knows it)
+  uint64_t origin;   // chain origin: first cut position (0, Advance target, shard start)
+  uint64_t min_pos;  // candidates below this absolute position are not real windows
+  uint64_t* d_out;   // device output
+  uint64_t out_cap;
+  bool dense;        // dense-candidate path
+  uint64_t halo0 = 0;  // readable bytes before the first piece (shards)
+};
+
+static int reset_state(dsx_ctx* c, uint64_t carry) {
+  c->npiece_call = 0;
+  DevState s{};
+  s.carry = carry;
+  *c->h_state = s;
+  HIPCHK(c, hipMemcpyAsync(c->state.p, c->h_state, sizeof(DevState), hipMemcpyHostToDevice,
+                           c->stream));
+  return DSX_OK;
+}
+
+static int read_state(dsx_ctx* c, DevState* out) {
+  HIPCHK(c, hipMemcpyAsync(c->h_state, c->state.p, sizeof(DevState), hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *out = *c->h_state;
+  return DSX_OK;
+}
+
+// Enqueue scan + stitch for one piece [P, P+len) whose bytes are at d_piece
+// (with `halo` readable bytes before it).
+static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_t halo,
+                         uint64_t P, uint64_t len, bool is_last) {
+  const dsx_params_t* p = cc.p;
+  // ---- scan geometry: balance regions over the persistent grid ----
+  const uint64_t slots_total = (uint64_t)c->ncu * kScanWaves;  // wave slots
+  uint32_t S, LS;
+  if (cc.dense) {
+    S = kDenseS;
+    LS = kDenseS;
+  } else {
+    const uint64_t per_lane = (len + slots_total * 64 - 1) / (slots_total * 64);
+    const uint64_t k = (per_lane + kMaxLaneBytes - 1) / kMaxLaneBytes;  // region rounds
+    uint64_t s = (len + k * slots_total * 64 - 1) / (k * slots_total * 64);
+    s = (s + kRound - 1) / kRound * kRound;
+    if (s < 48u * 16u) s = 48u * 16u;
+    if (s > kMaxLaneBytes) s = kMaxLaneBytes;
+    S = (uint32_t)s;
+    LS = kLaneSlots;
+  }
+  const uint64_t region_bytes = 64ull * S;
+  const uint64_t nregions = len == 0 ? 0 : (len + region_bytes - 1) / region_bytes;
+  const uint64_t nlanes = nregions * 64;
+  HIPCHK(c, grow(c, c->lane_cnt, nlanes));
+  HIPCHK(c, grow(c, c->lane_slot, nlanes * LS));
+  HIPCHK(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), c->stream));
+
+  ScanArgs sa{};
+  sa.base = d_piece;
+  sa.halo = halo;
+  sa.piece_abs = P;
+  sa.len = len;
+  sa.lane_bytes = S;
+  sa.rounds = S / kRound;
+  sa.nregions = (uint32_t)nregions;
+  sa.tc = make_tc(p);
+  sa.min_pos = cc.min_pos;
+  sa.lane_slots = LS;
+  sa.lane_cnt = c->lane_cnt.p;
+  sa.lane_slot = c->lane_slot.p;
+  sa.overflow = c->overflow.p;
+  const uint32_t pi = c->npiece_call++;
+  while (c->pev.size() < 3 * (size_t)(pi + 1)) {
+    hipEvent_t e;
+    HIPCHK(c, hipEventCreate(&e));
+    c->pev.push_back(e);
+  }
+  HIPCHK(c, hipEventRecord(c->pev[3 * pi], c->stream));
+  if (nregions > 0) {
+    const uint64_t need_wg = (nregions + kScanWaves - 1) / kScanWaves;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)c->ncu);
+    if (pick_mode(c, p->discriminator) == 1)
+      hipLaunchKernelGGL(scan_kernel<1>, dim3(grid), dim3(kScanThreads), 0, c->stream, sa);
+    else
+      hipLaunchKernelGGL(scan_kernel<0>, dim3(grid), dim3(kScanThreads), 0, c->stream, sa);
+    HIPCHK(c, hipGetLastError());
+  }
+
+  HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));
+  // ---- stitch geometry ----
+  StitchArgs ta{};
+  ta.chain.min = p->min;
+  ta.chain.max = p->max;
+  ta.chain.L = cc.L;
+  ta.chain.PE = P + len;
+  ta.chain.is_last = is_last ? 1u : 0u;
+  ta.pc.P = P;
+  ta.pc.nlanes = nlanes;
+  ta.pc.S = S;
+  ta.pc.lane_slots = LS;
+  ta.pc.lane_cnt = c->lane_cnt.p;
+  ta.pc.lane_slot = c->lane_slot.p;
+  ta.pc.overflow = c->overflow.p;
+  // the carried cut lies in (P - max, P] (its successor needed bytes >= P)
+  const uint64_t anchor = (P > cc.origin + p->max) ? P - p->max : cc.origin;
+  const uint64_t seg = std::max<uint64_t>(8 * p->max, 1ull << 20);
+  const uint64_t end = is_last ? cc.L : P + len;
+  const uint64_t nseg = end > anchor ? (end - anchor + seg - 1) / seg : 1;
+  ta.anchor = anchor;
+  ta.seg = seg;
+  ta.nseg = (uint32_t)nseg;
+  const double exp_per_seg = (double)seg / (double)p->discriminator + 8.0;
+  uint64_t spg = (uint64_t)((double)kWalkLdsCap / (2.0 * exp_per_seg)) - 1;
+  spg = std::max<uint64_t>(1, std::min<uint64_t>(spg, kMaxSpg));
+  ta.spg = (uint32_t)spg;
+  ta.lds_cap = kWalkLdsCap;
+  ta.scap = (uint32_t)(seg / p->min + 3);
+  HIPCHK(c, grow(c, c->seg_info, nseg));
+  HIPCHK(c, grow(c, c->stage, nseg * ta.scap));
+  HIPCHK(c, grow(c, c->rep, nseg * ta.scap));
+  HIPCHK(c, grow(c, c->rep_cnt, nseg));
+  HIPCHK(c, grow(c, c->rep_from, nseg));
+  HIPCHK(c, grow(c, c->flag_list, nseg));
+  HIPCHK(c, grow(c, c->out_off, nseg));
+  ta.seg_info = c->seg_info.p;
+  ta.stage = c->stage.p;
+  ta.rep = c->rep.p;
+  ta.rep_cnt = c->rep_cnt.p;
+  ta.rep_from = c->rep_from.p;
+  ta.flag_list = c->flag_list.p;
+  ta.out_off = c->out_off.p;
+  ta.out = cc.d_out;
+  ta.out_cap = cc.out_cap;
+  ta.state = c->state.p;
+  const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
+  const size_t walk_lds = (size_t)kWalkLdsCap * 4 + (kMaxSpg + 1) * 8;
+  hipLaunchKernelGGL(walk_kernel, dim3(walk_grid), dim3(256), walk_lds, c->stream, ta);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(fixup_kernel, dim3(1), dim3(1024), 0, c->stream, ta);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(gather_kernel, dim3((uint32_t)nseg), dim3(256), 0, c->stream, ta);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->pev[3 * pi + 2], c->stream));
+  c->stats.pieces++;
+  return DSX_OK;
+}
+
+// Runs a whole device-resident blob [origin.., origin+len) through the engine.
+static int run_device(dsx_ctx* c, const uint8_t* d_blob, uint64_t len, CallCfg cc) {
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = reset_state(c, cc.origin);
+  if (rc) return rc;
+  const uint64_t piece = cc.dense ? kDensePiece : kPieceMax;
+  for (uint64_t off = 0; off < len; off += piece) {
+    if (c->cancel.load()) return DSX_E_INTERRUPTED;
+    const uint64_t n = std::min(piece, len - off);
+    rc = enqueue_piece(c, cc, d_blob + off, off + cc.halo0, cc.origin + off, n, off + n == len);
+    if (rc) return rc;
+  }
+  return DSX_OK;
+}
+
+static int ensure_attr_walk(dsx_ctx* c) {
+  static bool done = false;
+  if (!done) {
+    HIPCHK(c, hipFuncSetAttribute((const void*)walk_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kWalkLdsCap * 4 + (kMaxSpg + 1) * 8)));
+    done = true;
+  }
+  return DSX_OK;
+}
+
+static int finish_call(dsx_ctx* c, uint64_t* n_out, uint64_t cap, bool* dense_retry) {
+  DevState s;
+  int rc = read_state(c, &s);
+  if (rc) return rc;
+  *dense_retry = false;
+  if (s.err & kErrDense) {
+    *dense_retry = true;
+    return DSX_OK;
+  }
+  c->stats.chunks = s.total;
+  c->stats.repaired_segments = s.repaired;
+  float scan = 0, stitch = 0;
+  for (uint32_t i = 0; i < c->npiece_call; ++i) {
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, c->pev[3 * i], c->pev[3 * i + 1]);
+    (void)hipEventElapsedTime(&b, c->pev[3 * i + 1], c->pev[3 * i + 2]);
+    scan += a;
+    stitch += b;
+  }
+  c->stats.scan_ms = scan;
+  c->stats.stitch_ms = stitch;
+  *n_out = s.total;
+  if ((s.err & kErrCapacity) || s.total > cap) return DSX_E_CAPACITY;
+  return DSX_OK;
+}
+
+extern "C" int dsx_sync(dsx_ctx_t* c) {
+  if (!c) return DSX_E_INVAL;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return DSX_OK;
+}
+
+extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, const dsx_params_t* p,
+                              uint64_t* out_ends, uint64_t cap, uint64_t* n_out, uint32_t flags);
+
+extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
+  if (!c || !n_out) return DSX_E_INVAL;
+  if (!c->pend.active) return DSX_E_STATE;
+  c->pend.active = false;
+  bool dense = false;
+  int rc = finish_call(c, n_out, c->pend.cap, &dense);
+  if (dense) {  // rare: redo on the dense-candidate path, synchronously
+    c->stats.dense_fallbacks++;
+    dsx_params_t p = c->pend.p;
+    return dsx_cut_device(c, c->pend.d_blob, c->pend.len, &p, c->pend.out, c->pend.cap, n_out,
+                          DSX_OUT_DEVICE);
+  }
+  return rc;
+}
+
+extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, const dsx_params_t* p,
+                              uint64_t* out_ends, uint64_t cap, uint64_t* n_out, uint32_t flags) {
+  if (!c || !p || !n_out || (len && !d_blob) || (cap && !out_ends)) return DSX_E_INVAL;
+  c->cancel.store(0);
+  int rc = ensure_attr_walk(c);
+  if (rc) return rc;
+  *n_out = 0;
+  if (len == 0) return DSX_OK;  // TestChunkerEmptyFile: no chunks
+  const bool dev_out = (flags & DSX_OUT_DEVICE) != 0;
+  const uint64_t need = len / p->min + 2;
+  if ((flags & DSX_NO_SYNC) && dev_out) {
+    CallCfg cc{p, len, 0, kRound, out_ends, cap, false};
+    c->pend.active = true;
+    c->pend.d_blob = d_blob;
+    c->pend.len = len;
+    c->pend.cap = cap;
+    c->pend.p = *p;
+    c->pend.out = out_ends;
+    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
+    rc = run_device(c, (const uint8_t*)d_blob, len, cc);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
+    return DSX_OK;
+  }
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    CallCfg cc{p, len, 0, kRound, nullptr, 0, attempt == 1};
+    if (dev_out) {
+      cc.d_out = out_ends;
+      cc.out_cap = cap;
+    } else {
+      HIPCHK(c, grow(c, c->out, need));
+      cc.d_out = c->out.p;
+      cc.out_cap = need;
+    }
+    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
+    rc = run_device(c, (const uint8_t*)d_blob, len, cc);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
+    bool dense = false;
+    rc = finish_call(c, n_out, dev_out ? cap : need, &dense);
+    if (dense) {
+      c->stats.dense_fallbacks++;
+      continue;
+    }
+    if (rc) return rc;
+    if (!dev_out && *n_out > cap) return DSX_E_CAPACITY;
+    if (!dev_out && *n_out) {
+      HIPCHK(c, hipMemcpy(out_ends, c->out.p, *n_out * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
+    return DSX_OK;
+  }
+  c->err = "dense-candidate path overflowed";
+  return DSX_E_INTERNAL;
+}
+
+// Host-resident pipeline: chunks of kHostChunk bytes are staged in pinned
+// memory and copied on copy_stream while the previous chunk is processed.
+static int run_host_pipeline(dsx_ctx* c, const dsx_params_t* p, uint64_t len,
+                             int (*fill)(void* ud, uint8_t* dst, uint64_t off, uint64_t n),
+                             void* ud, uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
+  HIPCHK(c, hipSetDevice(c->device));
+  c->cancel.store(0);
+  int rc = ensure_attr_walk(c);
+  if (rc) return rc;
+  *n_out = 0;
+  if (len == 0) return DSX_OK;
+  const uint64_t need = len / p->min + 2;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const bool dense = attempt == 1;
+    const uint64_t chunk = dense ? kDensePiece : std::min<uint64_t>(kHostChunk, len);
+    const uint64_t buf_sz = chunk + 64;
+    if (c->pinned_sz < buf_sz) {
+      for (auto& b : c->pinned) {
+        if (b) (void)hipHostFree(b);
+        b = nullptr;
+        HIPCHK(c, hipHostMalloc((void**)&b, buf_sz));
+      }
+      c->pinned_sz = buf_sz;
+    }
+    HIPCHK(c, grow(c, c->dbuf[0], buf_sz));
+    HIPCHK(c, grow(c, c->dbuf[1], buf_sz));
+    HIPCHK(c, grow(c, c->out, need));
+    CallCfg cc{p, len, 0, kRound, c->out.p, need, dense};
+    rc = reset_state(c, 0);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
+    uint64_t i = 0;
+    for (uint64_t off = 0; off < len; off += chunk, ++i) {
+      if (c->cancel.load()) return DSX_E_INTERRUPTED;
+      const int b = (int)(i & 1);
+      const uint64_t n = std::min(chunk, len - off);
+      const uint64_t h = std::min<uint64_t>(64, off);
+      // the pinned buffer b was last used by the copy two chunks ago
+      if (i >= 2) HIPCHK(c, hipEventSynchronize(c->copy_done[b]));
+      rc = fill(ud, c->pinned[b], off - h, n + h);
+      if (rc) return rc;
+      // device buffer b was last read by the compute two chunks ago
+      if (i >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->comp_done[b], 0));
+      HIPCHK(c, hipMemcpyAsync(c->dbuf[b].p, c->pinned[b], n + h, hipMemcpyHostToDevice,
+                               c->copy_stream));
+      HIPCHK(c, hipEventRecord(c->copy_done[b], c->copy_stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->copy_done[b], 0));
+      rc = enqueue_piece(c, cc, c->dbuf[b].p + h, h, off, n, off + n == len);
+      if (rc) return rc;
+      HIPCHK(c, hipEventRecord(c->comp_done[b], c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
+    bool dn = false;
+    rc = finish_call(c, n_out, need, &dn);
+    if (dn) {
+      c->stats.dense_fallbacks++;
+      continue;
+    }
+    if (rc) return rc;
+    if (*n_out > cap) return DSX_E_CAPACITY;
+    if (*n_out)
+      HIPCHK(c, hipMemcpy(out_ends, c->out.p, *n_out * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return DSX_OK;
+  }
+  c->err = "dense-candidate path overflowed";
+  return DSX_E_INTERNAL;
+}
+
+struct MemSrc {
+  const uint8_t* p;
+};
+static int fill_mem(void* ud, uint8_t* dst, uint64_t off, uint64_t n) {
+  memcpy(dst, ((MemSrc*)ud)->p + off, n);
+  return DSX_OK;
+}
+struct FdSrc {
+  int fd;
+  uint64_t base;
+};
+static int fill_fd(void* ud, uint8_t* dst, uint64_t off, uint64_t n) {
+  FdSrc* s = (FdSrc*)ud;
+  uint64_t got = 0;
+  while (got < n) {
+    const ssize_t r = pread(s->fd, dst + got, n - got, (off_t)(s->base + off + got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return DSX_E_IO;
+    }
+    if (r == 0) return DSX_E_IO;  // file shrank underneath us
+    got += (uint64_t)r;
+  }
+  return DSX_OK;
+}
+
+extern "C" int dsx_cut_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, const dsx_params_t* p,
+                            uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
+  if (!c || !p || !n_out || (len && !h_blob) || (cap && !out_ends)) return DSX_E_INVAL;
+  MemSrc s{(const uint8_t*)h_blob};
+  return run_host_pipeline(c, p, len, fill_mem, &s, out_ends, cap, n_out);
+}
+
+extern "C" int dsx_cut_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, const dsx_params_t* p,
+                          uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
+  if (!c || !p || !n_out || fd < 0 || (cap && !out_ends)) return DSX_E_INVAL;
+  if (len == UINT64_MAX) {
+    const off_t end = lseek(fd, 0, SEEK_END);
+    if (end < 0) return DSX_E_IO;
+    len = (uint64_t)end > off ? (uint64_t)end - off : 0;
+  }
+  FdSrc s{fd, off};
+  return run_host_pipeline(c, p, len, fill_fd, &s, out_ends, cap, n_out);
+}
+
+// --------------------------------------------------------------------------
+// streaming: Chunker.Next / Advance over an io.Reader (chunker.go:206-309)
+// --------------------------------------------------------------------------
+extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
+  if (!c || !p) return DSX_E_INVAL;
+  c->st = dsx_ctx::Stream();
+  c->st.active = true;
+  c->st.p = *p;
+  return ensure_attr_walk(c);
+}
+
+// Scan everything pushed so far (one piece) and append the confirmed cuts.
+static int stream_process(dsx_ctx* c) {
+  auto& s = c->st;
+  const uint64_t buf_end = s.buf_pos + s.buf.size();
+  if (buf_end <= s.scan_pos && !(s.eof && !s.done)) return DSX_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t len = buf_end - s.scan_pos;
+  if (len == 0 && s.eof) {
+    // end of input exactly at the scanned position: finish the chain
+    if (s.carry < buf_end) {
+      // successor of carry is the tail (len - carry <= max here, no candidates left)
+      s.cuts.push_back(buf_end);
+      s.carry = buf_end;
+    }
+    s.done = true;
+    return DSX_OK;
+  }
+  // bytes kept before scan_pos (never before the chain origin: those are
+  // virtual zeros for the scan)
+  const uint64_t halo = std::min<uint64_t>(64, s.scan_pos - std::max(s.buf_pos, s.origin));
+  HIPCHK(c, grow(c, c->dbuf[0], len + 64));
+  HIPCHK(c, hipMemcpyAsync(c->dbuf[0].p, s.buf.data() + (s.scan_pos - halo - s.buf_pos),
+                           len + halo, hipMemcpyHostToDevice, c->stream));
+  const uint64_t need = (buf_end - s.carry) / s.p.min + 4;
+  HIPCHK(c, grow(c, c->out, need));
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    CallCfg cc{&s.p, buf_end, s.origin, s.origin + kRound, c->out.p, need, attempt == 1};
+    int rc = reset_state(c, s.carry);
+    if (rc) return rc;
+    if (!cc.dense) {
+      rc = enqueue_piece(c, cc, c->dbuf[0].p + halo, halo, s.scan_pos, len, s.eof);
+      if (rc) return rc;
+    } else {
+      for (uint64_t o = 0; o < len; o += kDensePiece) {
+        const uint64_t n = std::min(kDensePiece, len - o);
+        rc = enqueue_piece(c, cc, c->dbuf[0].p + halo + o, halo + o, s.scan_pos + o, n,
+                           s.eof && o + n == len);
+        if (rc) return rc;
+      }
+    }
+    DevState st;
+    rc = read_state(c, &st);
+    if (rc) return rc;
+    if (st.err & kErrDense) {
+      c->stats.dense_fallbacks++;
+      continue;
+    }
+    if (st.err) {
+      c->err = "stream: stitch error";
+      return DSX_E_INTERNAL;
+    }
+    if (st.total) {
+      std::vector<uint64_t> v(st.total);
+      HIPCHK(c, hipMemcpy(v.data(), c->out.p, st.total * 8, hipMemcpyDeviceToHost));
+      for (uint64_t x : v) s.cuts.push_back(x);
+    }
+    s.carry = st.carry;
+    s.scan_pos = buf_end;
+    if (s.eof) s.done = true;
+    return DSX_OK;
+  }
+  c->err = "dense-candidate path overflowed";
+  return DSX_E_INTERNAL;
+}
+
+extern "C" int dsx_stream_push(dsx_ctx_t* c, const void* bytes, uint64_t len, int eof) {
+  if (!c || (len && !bytes)) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active || s.eof) return DSX_E_STATE;
+  const uint8_t* b = (const uint8_t*)bytes;
+  if (s.skip) {  // Advance() beyond the buffered bytes drops future input
+    const uint64_t d = std::min(s.skip, len);
+    s.skip -= d;
+    b += d;
+    len -= d;
+  }
+  // compact: keep bytes from min(cur, scan_pos - 64)
+  uint64_t keep_from = std::min(s.cur, s.scan_pos >= 64 ? s.scan_pos - 64 : 0);
+  keep_from = std::max(keep_from, s.buf_pos);
+  if (keep_from > s.buf_pos) {
+    s.buf.erase(s.buf.begin(), s.buf.begin() + (keep_from - s.buf_pos));
+    s.buf_pos = keep_from;
+  }
+  s.last_chunk = nullptr;
+  s.buf.insert(s.buf.end(), b, b + len);
+  if (eof) s.eof = true;
+  const uint64_t pending = s.buf_pos + s.buf.size() - s.scan_pos;
+  if (pending >= kStreamBatch || s.eof) return stream_process(c);
+  return DSX_OK;
+}
+
+extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
+  if (!c || !start || !size) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active) return DSX_E_STATE;
+  if (s.cuts.empty()) {
+    *start = s.cur;
+    *size = 0;
+    return 0;
+  }
+  const uint64_t e = s.cuts.front();
+  s.cuts.pop_front();
+  *start = s.cur;
+  *size = e - s.cur;
+  s.last_chunk = s.buf.data() + (s.cur - s.buf_pos);
+  s.cur = e;
+  return 1;
+}
+
+extern "C" const uint8_t* dsx_stream_chunk_data(dsx_ctx_t* c) { return c ? c->st.last_chunk : nullptr; }
+
+extern "C" int dsx_stream_done(dsx_ctx_t* c) {
+  if (!c) return 0;
+  return c->st.active && c->st.done && c->st.cuts.empty() ? 1 : 0;
+}
+
+extern "C" int dsx_stream_advance(dsx_ctx_t* c, uint64_t n) {
+  if (!c) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active) return DSX_E_STATE;
+  const uint64_t target = s.cur + n;
+  const uint64_t buf_end = s.buf_pos + s.buf.size();
+  s.cuts.clear();
+  s.last_chunk = nullptr;
+  if (target <= buf_end) {
+    s.buf.erase(s.buf.begin(), s.buf.begin() + (target - s.buf_pos));
+    s.skip = 0;
+  } else {
+    s.buf.clear();
+    s.skip = target - buf_end;
+  }
+  s.buf_pos = target;
+  s.scan_pos = target;
+  s.origin = target;
+  s.cur = target;
+  s.carry = target;
+  s.done = false;
+  if (s.eof) {
+    s.skip = 0;
+    return stream_process(c);  // remaining buffered bytes form the rest of the stream
+  }
+  return DSX_OK;
+}
+
+// --------------------------------------------------------------------------
+// synthetic data
+// --------------------------------------------------------------------------
+extern "C" int dsx_gen_uniform(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_t len,
+                               uint64_t seed) {
+  if (!c || (len && !d_dst)) return DSX_E_INVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!len) return DSX_OK;
+  const uint64_t threads = (len + 15) / 16;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((threads + 255) / 256, 65536);
+  hipLaunchKernelGGL(gen_uniform_kernel, dim3(grid), dim3(256), 0, c->stream, (uint8_t*)d_dst,
+                     offset, len, seed);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return DSX_OK;
+}
+
+extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_t len,
+                             uint64_t seed, double p_repeat) {
+  if (!c || (len && !d_dst) || !(p_repeat >= 0.0 && p_repeat < 1.0)) return DSX_E_INVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!len) return DSX_OK;
+  const uint32_t thresh = (uint32_t)std::min(4294967295.0, p_repeat * 4294967296.0);
+  const uint64_t threads = (len + 15) / 16;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((threads + 255) / 256, 65536);
+  hipLaunchKernelGGL(gen_dedup_kernel, dim3(grid), dim3(256), 0, c->stream, (uint8_t*)d_dst,
+                     offset, len, seed, thresh);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return DSX_OK;
+}
+
+// --------------------------------------------------------------------------
+// diagnostics: GPU boundary predicate vs h % d == d-1
+// --------------------------------------------------------------------------
+extern "C" int dsx_selftest_boundary(dsx_ctx_t* c, const dsx_params_t* p, int mode, uint64_t h0,
+                                     uint64_t n, uint64_t* mismatches) {
+  if (!c || !p || !mismatches) return DSX_E_INVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (mode < 0) mode = pick_mode(c, p->discriminator);
+  DevBuf<unsigned long long> m;
+  HIPCHK(c, m.ensure(1));
+  HIPCHK(c, hipMemsetAsync(m.p, 0, 8, c->stream));
+  hipLaunchKernelGGL(boundary_selftest_kernel, dim3(4096), dim3(256), 0, c->stream, make_tc(p),
+                     mode, h0, n, m.p);
+  HIPCHK(c, hipGetLastError());
+  unsigned long long v = 0;
+  HIPCHK(c, hipMemcpyAsync(&v, m.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  m.release();
+  *mismatches = v;
+  return DSX_OK;
+}
+
+// --------------------------------------------------------------------------
+// multi-GPU shards (split-and-align across ranks, make.go:22-163 / 277-327)
+// --------------------------------------------------------------------------
+extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
+                               uint64_t shard_start, uint64_t shard_len, uint64_t total,
+                               const dsx_params_t* p, dsx_seam_t* seam) {
+  if (!c || !p || !seam || (shard_len && !d_shard) || shard_start + shard_len > total)
+    return DSX_E_INVAL;
+  if (shard_start > 0 && halo < kRound) return DSX_E_INVAL;
+  c->cancel.store(0);
+  int rc = ensure_attr_walk(c);
+  if (rc) return rc;
+  memset(seam, 0, sizeof *seam);
+  seam->shard_start = shard_start;
+  seam->shard_len = shard_len;
+  seam->total = total;
+  seam->first_cand_beyond = UINT64_MAX;
+  c->shard_start = shard_start;
+  c->shard_len = shard_len;
+  c->shard_min = p->min;
+  c->shard_max = p->max;
+  const bool is_last = shard_start + shard_len == total;
+  const uint64_t need = shard_len / p->min + 4;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    HIPCHK(c, grow(c, c->out, need));
+    CallCfg cc{p, total, shard_start, kRound, c->out.p, need, attempt == 1};
+    cc.halo0 = shard_start > 0 ? halo : 0;
+    // the speculative chain starts at the virtual cut shard_start; the piece
+    // is final only for the last shard
+    HIPCHK(c, hipSetDevice(c->device));
+    rc = reset_state(c, shard_start);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
+    const uint64_t piece = cc.dense ? kDensePiece : kPieceMax;
+    for (uint64_t off = 0; off < shard_len; off += piece) {
+      const uint64_t n = std::min(piece, shard_len - off);
+      rc = enqueue_piece(c, cc, (const uint8_t*)d_shard + off, off + cc.halo0, shard_start + off,
+                         n, is_last && off + n == shard_len);
+      if (rc) return rc;
+    }
+    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
+    DevState st;
+    rc = read_state(c, &st);
+    if (rc) return rc;
+    if (st.err & kErrDense) {
+      c->stats.dense_fallbacks++;
+      continue;
+    }
+    if (st.err) {
+      c->err = "shard: stitch error";
+      return DSX_E_INTERNAL;
+    }
+    c->shard_cuts.resize(st.total);
+    if (st.total)
+      HIPCHK(c, hipMemcpy(c->shard_cuts.data(), c->out.p, st.total * 8, hipMemcpyDeviceToHost));
+    seam->exit_cut = st.carry;
+    // seam window: candidates and spec cuts of the shard's first bytes
+    uint64_t wend = shard_start + std::min<uint64_t>(shard_len, 32 * p->max);
+    // candidates in (shard_start, wend]: they come from the last piece scanned only
+    // when the shard fits one piece; rescan the window as its own piece otherwise
+    std::vector<uint64_t> cands;
+    {
+      const uint64_t wlen = wend - shard_start;
+      CallCfg wc{p, total, shard_start, kRound, c->out.p, need, true};
+      wc.halo0 = cc.halo0;
+      rc = reset_state(c, shard_start);
+      if (rc) return rc;
+      rc = enqueue_piece(c, wc, (const uint8_t*)d_shard, wc.halo0, shard_start, wlen,
+                         is_last && wlen == shard_len);
+      if (rc) return rc;
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      // read back lane lists of the dense-path scan of the window
+      const uint64_t S = kDenseS;
+      const uint64_t nl = (wlen + 64 * S - 1) / (64 * S) * 64;
+      std::vector<uint32_t> cnt(nl);
+      std::vector<uint16_t> sl(nl * S);
+      HIPCHK(c, hipMemcpy(cnt.data(), c->lane_cnt.p, nl * 4, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(sl.data(), c->lane_slot.p, nl * S * 2, hipMemcpyDeviceToHost));
+      for (uint64_t g = 0; g < nl; ++g)
+        for (uint32_t i = 0; i < cnt[g] && i < S; ++i) cands.push_back(shard_start + g * S + sl[g * S + i]);
+    }
+    if (cands.size() > DSX_SEAM_MAX_CANDS) {
+      seam->first_cand_beyond = cands[DSX_SEAM_MAX_CANDS];
+      wend = cands[DSX_SEAM_MAX_CANDS - 1];
+      cands.resize(DSX_SEAM_MAX_CANDS);
+    }
+    uint32_t nc = 0;
+    for (uint64_t x : c->shard_cuts) {
+      if (x > wend) break;
+      if (nc == DSX_SEAM_MAX_CUTS) {
+        wend = seam->cuts[nc - 1];
+        break;
+      }
+      seam->cuts[nc++] = x;
+    }
+    uint32_t ncand = 0;
+    for (uint64_t x : cands)
+      if (x <= wend) seam->cands[ncand++] = x;
+    seam->ncands = ncand;
+    seam->ncuts = nc;
+    seam->window_end = wend;
+    seam->flags = is_last ? 1u : 0u;
+    return DSX_OK;
+  }
+  c->err = "dense-candidate path overflowed";
+  return DSX_E_INTERNAL;
+}
+
+extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks, int rank,
+                                 uint64_t* out_ends, uint64_t cap, uint64_t* n_out,
+                                 uint32_t flags) {
+  if (!c || !all || nranks < 1 || rank < 0 || rank >= nranks || !n_out) return DSX_E_INVAL;
+  (void)flags;
+  HIPCHK(c, hipSetDevice(c->device));
+  const dsx_params_t* pp = nullptr;
+  (void)pp;
+  DevBuf<dsx_seam_t> d_all;
+  DevBuf<uint64_t> d_out, d_info;
+  HIPCHK(c, d_all.ensure(nranks));
+  HIPCHK(c, d_out.ensure(DSX_SEAM_MAX_CUTS + 4));
+  HIPCHK(c, d_info.ensure(8));
+  HIPCHK(c, hipMemcpyAsync(d_all.p, all, sizeof(dsx_seam_t) * nranks, hipMemcpyHostToDevice,
+                           c->stream));
+  hipLaunchKernelGGL(seam_resolve_kernel, dim3(1), dim3(64), 0, c->stream, d_all.p, nranks, rank,
+                     c->shard_min, c->shard_max, d_out.p, d_info.p);
+  HIPCHK(c, hipGetLastError());
+  uint64_t info[8];
+  HIPCHK(c, hipMemcpyAsync(info, d_info.p, sizeof info, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // info: [0]=status (0 ok, else failing seam + 1), [1]=entry cut c_r, [2]=#ext cuts
+  if (info[0] != 0) {
+    char b[160];
+    snprintf(b, sizeof b, "seam %llu did not converge inside its window",
+             (unsigned long long)(info[0] - 1));
+    c->err = b;
+    d_all.release(); d_out.release(); d_info.release();
+    return DSX_E_INTERNAL;
+  }
+  std::vector<uint64_t> ext(info[2]);
+  if (info[2]) HIPCHK(c, hipMemcpy(ext.data(), d_out.p, info[2] * 8, hipMemcpyDeviceToHost));
+  d_all.release(); d_out.release(); d_info.release();
+  // this rank's cuts: ext cuts in (start, c_r) followed by spec cuts >= c_r
+  const uint64_t cr = info[1];
+  uint64_t n = 0;
+  std::vector<uint64_t> res;
+  res.reserve(ext.size() + c->shard_cuts.size());
+  for (uint64_t x : ext) res.push_back(x);
+  for (uint64_t x : c->shard_cuts)
+    if (x >= cr) res.push_back(x);
+  n = res.size();
+  *n_out = n;
+  if (n > cap) return DSX_E_CAPACITY;
+  if (n) memcpy(out_ends, res.data(), n * 8);
+  return DSX_OK;
+}

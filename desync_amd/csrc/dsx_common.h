@@ -1,0 +1,63 @@
+// dsx_common.h -- shared device/host definitions of the MI355X chunker.
+//
+// Terms (desync's domain):
+//   candidate  position p whose 48-byte window [p-48,p) hashes to H(p) with
+//              H(p) % d == d-1 (chunker.go:265-268); depends on p only.
+//   cut        chunk end offset on the chain 0 -> next(0) -> ... -> len.
+//   piece      contiguous byte range scanned by one scan launch.
+//   lane seg   S contiguous bytes owned by one wavefront lane in the scan.
+//   region     64 consecutive lane segments (one wavefront's work unit).
+//   segment    stitch work unit: SEG bytes of cut-chain positions.
+#pragma once
+#include <stdint.h>
+
+namespace dsx {
+
+constexpr int kWave = 64;
+// ---- scan kernel geometry (see DESIGN.md "Scan kernel") --------------------
+constexpr int kScanWaves = 8;                 // waves per workgroup (2 per SIMD)
+constexpr int kScanThreads = kScanWaves * kWave;
+constexpr int kRound = 48;                    // bytes per lane per round == window
+constexpr int kNBuf = 4;                      // LDS staging ring depth per wave
+constexpr int kStageBytes = kWave * kRound;   // 3072 B per staging buffer
+constexpr int kTableBytes = 256 * 256;        // 256 byte values x 32 lane slots x {T,Trot}
+constexpr int kScanLds = kTableBytes + kScanWaves * kNBuf * kStageBytes;  // 163840
+constexpr int kLaneSlots = 32;                // candidate slots per lane segment
+constexpr uint32_t kMaxLaneBytes = 48u * 1365u;  // keeps slot offsets in u16
+
+static_assert(kScanLds <= 163840, "scan LDS budget exceeds 160 KiB");
+
+// Division-free boundary test constants (host-computed, chunker.go:147-170).
+struct TestConsts {
+  uint32_t d;      // discriminator
+  uint32_t dm1;    // d - 1
+  uint32_t inv;    // inverse of odd part of d mod 2^32
+  uint32_t qmax;   // (2^32-1)/d - qbias
+  uint32_t qbias;
+  uint32_t rot;    // k = ctz(d): rotate right by k
+  float rcp;       // fl(1/d)
+  float c0;        // fl(0.5 - (d-1)/d)
+};
+
+struct ScanArgs {
+  const uint8_t* base;   // device pointer of the piece's first byte
+  uint64_t halo;         // readable bytes before base (0 only at blob start)
+  uint64_t piece_abs;    // absolute blob position of base[0]
+  uint64_t len;          // piece length in bytes
+  uint32_t lane_bytes;   // S, multiple of kRound
+  uint32_t rounds;       // S / kRound
+  uint32_t nregions;     // ceil(len / (64*S))
+  uint32_t pad;
+  TestConsts tc;
+  uint64_t min_pos;      // candidates at absolute p < min_pos are dropped (origin + 49)
+  uint32_t lane_slots;   // slot capacity per lane (kLaneSlots, or S on the dense path)
+  uint32_t pad2;
+  uint32_t* lane_cnt;    // [nregions*64] candidates per lane segment (exact)
+  uint16_t* lane_slot;   // [nregions*64*lane_slots] offsets o in [1,S] (p = lane base + o)
+  uint32_t* overflow;    // number of lane segments with more than kLaneSlots
+};
+
+// Sentinel for "successor depends on bytes beyond the piece" (non-final piece).
+constexpr uint64_t kUndet = ~0ull;
+
+}  // namespace dsx

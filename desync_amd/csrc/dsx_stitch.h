@@ -1,0 +1,79 @@
+// dsx_stitch.h -- device structures shared by the stitch kernels and the host
+// engine (dsx_api.cpp).
+#pragma once
+#include <stdint.h>
+
+namespace dsx {
+
+// Where a piece's candidates live: per-lane slot lists written by the scan.
+// Lane gl covers positions (P + gl*S, P + (gl+1)*S]; candidate = base + slot.
+struct PieceCands {
+  uint64_t P;             // absolute position of the piece's first byte
+  uint64_t nlanes;
+  uint32_t S;             // lane segment bytes
+  uint32_t lane_slots;    // slot capacity per lane (LS)
+  const uint32_t* lane_cnt;
+  const uint16_t* lane_slot;
+  const uint32_t* overflow;
+};
+
+// Chain rule inputs (chunker.go:206-277): L is the blob length (known only on
+// the final piece), PE the absolute end of the scanned bytes.
+struct ChainParams {
+  uint64_t min, max;
+  uint64_t L;   // valid if is_last
+  uint64_t PE;  // piece end (absolute)
+  uint32_t is_last;
+  uint32_t pad;
+};
+
+struct SegInfo {
+  uint64_t E;      // entry cut used for staged(k) (= X_{k-1}, or s0 for k == 0)
+  uint64_t X;      // exit of the speculative chain started at seg_start(k)
+  uint64_t Z;      // exit of staged(k)
+  uint32_t cnt;    // cuts in staged(k)
+  uint32_t flags;  // kSeg*
+};
+constexpr uint32_t kSegEnd = 1u;       // staged chain reached the blob end
+constexpr uint32_t kSegUndet = 2u;     // stopped: successor beyond the piece
+constexpr uint32_t kSegDense = 4u;     // candidates did not fit LDS: repair walks it
+constexpr uint32_t kSegOverflow = 8u;  // more cuts than staging capacity
+
+// Chain state carried across pieces and kernels (device memory).
+struct DevState {
+  uint64_t carry;       // last true cut (chain position)
+  uint64_t total;       // cuts emitted so far in this call
+  uint64_t piece_cuts;  // cuts emitted by the current piece
+  uint64_t repaired;    // segments repaired (stats)
+  uint32_t done;        // chain reached the blob end
+  uint32_t err;         // kErr* bits
+  uint32_t active;      // current piece was processed (K3 ran its body)
+  uint32_t pad;
+};
+constexpr uint32_t kErrCapacity = 1u;  // output capacity exceeded
+constexpr uint32_t kErrDense = 2u;     // a lane overflowed its candidate slots
+
+constexpr uint32_t kMaxSpg = 255;  // segments per walk workgroup (+1 redundant)
+
+struct StitchArgs {
+  ChainParams chain;
+  PieceCands pc;
+  uint64_t anchor;   // seg_start(k) = anchor + k*seg for k >= 1
+  uint64_t seg;      // SEG bytes
+  uint32_t nseg;     // T
+  uint32_t spg;      // segments per K2 workgroup
+  uint32_t lds_cap;  // candidates per K2 workgroup (LDS)
+  uint32_t scap;     // cut capacity per segment (SEG/min + 2)
+  SegInfo* seg_info;
+  uint64_t* stage;   // [nseg * scap]
+  uint64_t* rep;     // [nseg * scap]
+  uint32_t* rep_cnt;
+  uint32_t* rep_from;
+  uint32_t* flag_list;
+  uint64_t* out_off;
+  uint64_t* out;     // contiguous cut list (device)
+  uint64_t out_cap;
+  DevState* state;
+};
+
+}  // namespace dsx

@@ -1,0 +1,487 @@
+// dsx_stitch.hip -- candidates -> cut chain, on the GPU.
+//
+// Reference semantics: the sequential chain of Chunker.Next()
+// (chunker.go:206-277): from a cut s the next cut is the tail end if
+// len-s <= min, else the first candidate in (s+min, s+min(len-s,max)], else
+// s+min(len-s,max).  make.go:22-163 parallelises this by starting workers at
+// span*i and aligning each with its successor (syncWith, make.go:277-327);
+// the result equals the sequential chain (make_test.go:16-80).
+//
+// GPU form of that split-and-align (DESIGN.md "Stitch"):
+//   segments  [seg_start(k), seg_end(k)) of SEG bytes; segment 0 starts at the
+//             true carried cut s0, segment k>0 at a virtual cut (make.go's
+//             worker start).
+//   K2 walk   per segment k (one lane each, candidates staged in LDS):
+//             X_k  = exit of the speculative chain started at seg_start(k)
+//                    (the last cut <= seg_end(k));
+//             staged(k) = cuts in (seg_start(k), seg_end(k)] of the chain that
+//                    enters from X_{k-1} (spec chain of the previous segment);
+//             Z_k  = last cut of staged(k).
+//             staged(k+1) is the true chain iff staged(k) is and X_k == Z_k
+//             (the two chains met inside segment k -- syncWith's test).
+//   K3 fixup  one workgroup: repairs the rare segments where X_k != Z_k by a
+//             sequential walk over global candidates until it rejoins the
+//             staged chain, then an exclusive scan of per-segment counts.
+//   K4 gather contiguous cut list.
+#include <hip/hip_runtime.h>
+
+#include "dsx_common.h"
+#include "dsx_stitch.h"
+
+namespace dsx {
+
+constexpr uint64_t kNone = ~0ull;
+
+// ---- candidate sources -----------------------------------------------------
+// Sorted candidates in LDS, positions lo + c[i].  first_in(a, b) returns the
+// first candidate in (a, b] or kNone; `a` must be non-decreasing across calls.
+struct LdsSrc {
+  const uint32_t* c;
+  uint32_t n;
+  uint32_t j;
+  uint64_t lo;
+  __device__ uint64_t first_in(uint64_t a, uint64_t b) {
+    const uint64_t ar = a - lo;  // a >= lo always (a = s+min, s >= lo)
+    while (j < n && (uint64_t)c[j] <= ar) ++j;
+    if (j < n) {
+      const uint64_t p = lo + c[j];
+      if (p <= b) return p;
+    }
+    return kNone;
+  }
+  // reset j to the first candidate > a (binary search)
+  __device__ void seek(uint64_t a) {
+    const uint64_t ar = a < lo ? 0 : a - lo;
+    uint32_t l = 0, h = n;
+    while (l < h) {
+      const uint32_t m = (l + h) >> 1;
+      if ((uint64_t)c[m] <= ar) l = m + 1; else h = m;
+    }
+    j = l;
+  }
+};
+
+// Candidates straight from the scan's per-lane slot lists (global memory);
+// used by the sequential repair only.
+struct GlobalSrc {
+  const PieceCands* pc;
+  __device__ uint64_t first_in(uint64_t a, uint64_t b) const {
+    // lane gl covers positions (P + gl*S, P + (gl+1)*S]
+    if (b <= pc->P) return kNone;
+    const uint64_t lo_pos = a < pc->P ? pc->P : a;
+    uint64_t gl = (lo_pos - pc->P) / pc->S;
+    const uint64_t gl_end = (b - pc->P - 1) / pc->S;
+    for (; gl <= gl_end && gl < pc->nlanes; ++gl) {
+      const uint32_t cnt = pc->lane_cnt[gl];
+      const uint32_t n = cnt < pc->lane_slots ? cnt : pc->lane_slots;
+      const uint64_t base = pc->P + gl * (uint64_t)pc->S;
+      const uint16_t* sl = pc->lane_slot + gl * (uint64_t)pc->lane_slots;
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t p = base + sl[i];
+        if (p > a) return p <= b ? p : kNone;
+      }
+    }
+    return kNone;
+  }
+};
+
+// One step of the chain rule.  Returns the next cut, or kUndet if it depends
+// on bytes beyond the piece end (non-final piece).
+template <class Src>
+__device__ __forceinline__ uint64_t next_cut(uint64_t s, Src& src, const ChainParams& w) {
+  uint64_t lim;
+  if (w.is_last) {
+    if (w.L - s <= w.min) return w.L;  // chunker.go:215-217
+    lim = s + w.max < w.L ? s + w.max : w.L;  // chunker.go:221
+  } else {
+    lim = s + w.max;
+  }
+  const uint64_t c = src.first_in(s + w.min, lim);  // chunker.go:259-271
+  if (c != kNone) return c;
+  if (!w.is_last && lim > w.PE) return kUndet;
+  return lim;  // chunker.go:276
+}
+
+__device__ __forceinline__ uint64_t seg_start(const StitchArgs& a, uint64_t s0, uint32_t k) {
+  return k == 0 ? s0 : a.anchor + (uint64_t)k * a.seg;
+}
+__device__ __forceinline__ uint64_t seg_end(const StitchArgs& a, uint32_t k) {
+  if (k + 1 >= a.nseg) return a.chain.is_last ? a.chain.L : a.chain.PE;
+  return a.anchor + (uint64_t)(k + 1) * a.seg;
+}
+
+// ---- K2: per-segment speculative walks ------------------------------------
+constexpr int kWalkThreads = 256;
+
+__global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* cand = smem;                         // [a.lds_cap]
+  uint64_t* xs = (uint64_t*)(smem + a.lds_cap);  // [kMaxSpg + 1] spec exits
+  __shared__ uint32_t s_part[kWalkThreads];
+  __shared__ uint32_t s_total;
+
+  const DevState* st = a.state;
+  if (st->done || *a.pc.overflow) return;  // finished, or scan slots overflowed
+  const uint64_t s0 = st->carry;
+  const uint32_t kA = blockIdx.x * a.spg;
+  if (kA >= a.nseg) return;
+  const uint32_t kB = (kA + a.spg < a.nseg ? kA + a.spg : a.nseg) - 1;  // inclusive
+  const uint32_t kFirst = kA > 0 ? kA - 1 : 0;                             // redundant walk
+  const uint64_t lo = seg_start(a, s0, kFirst);
+  const uint64_t hi = seg_end(a, kB);
+  const PieceCands& pc = a.pc;
+
+  // ---- gather candidates in (lo, hi] into LDS, sorted (lane order) ----
+  uint64_t gl0 = lo <= pc.P ? 0 : (lo - pc.P) / pc.S;
+  uint64_t gl1 = hi <= pc.P ? 0 : (hi - pc.P - 1) / pc.S + 1;  // exclusive
+  if (gl1 > pc.nlanes) gl1 = pc.nlanes;
+  if (gl0 > gl1) gl0 = gl1;
+  const uint64_t nl = gl1 - gl0;
+  const uint64_t per = (nl + kWalkThreads - 1) / kWalkThreads;
+  const uint64_t my0 = gl0 + (uint64_t)threadIdx.x * per;
+  const uint64_t my1 = (my0 + per < gl1) ? my0 + per : gl1;
+  uint32_t mine = 0;
+  for (uint64_t g = my0; g < my1; ++g) {
+    const uint32_t c = pc.lane_cnt[g];
+    mine += c < pc.lane_slots ? c : pc.lane_slots;
+  }
+  s_part[threadIdx.x] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // tiny serial scan over 256 partials
+    uint32_t acc = 0;
+    for (int i = 0; i < kWalkThreads; ++i) {
+      const uint32_t v = s_part[i];
+      s_part[i] = acc;
+      acc += v;
+    }
+    s_total = acc;
+  }
+  __syncthreads();
+  const uint32_t total = s_total;
+  const bool dense = total > a.lds_cap;
+  if (!dense) {
+    uint32_t o = s_part[threadIdx.x];
+    for (uint64_t g = my0; g < my1; ++g) {
+      const uint32_t c = pc.lane_cnt[g];
+      const uint32_t n = c < pc.lane_slots ? c : pc.lane_slots;
+      const uint64_t base = pc.P + g * (uint64_t)pc.S;
+      const uint16_t* sl = pc.lane_slot + g * (uint64_t)pc.lane_slots;
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t p = base + sl[i];
+        // keep the array sorted: below-range -> 0, above-range -> UINT32_MAX
+        cand[o++] = p <= lo ? 0u : (p > hi ? 0xFFFFFFFFu : (uint32_t)(p - lo));
+      }
+    }
+  }
+  __syncthreads();
+
+  const uint32_t nwalk = kB - kFirst + 1;
+  // ---- phase 1: speculative chain of each segment -> exit X_k ----
+  if (!dense && threadIdx.x < nwalk) {
+    const uint32_t k = kFirst + threadIdx.x;
+    const uint64_t v = seg_start(a, s0, k);
+    const uint64_t e = seg_end(a, k);
+    LdsSrc src{cand, total, 0, lo};
+    src.seek(v);
+    uint64_t x = v, last = v;
+    while (true) {
+      if (a.chain.is_last && x >= a.chain.L) break;
+      const uint64_t nx = next_cut(x, src, a.chain);
+      if (nx == kUndet || nx > e) break;
+      last = nx;
+      x = nx;
+    }
+    xs[threadIdx.x] = last;
+    if (k >= kA) a.seg_info[k].X = last;  // kA-1 belongs to the previous workgroup
+  }
+  __syncthreads();
+
+  // ---- phase 2: staged chain entering from X_{k-1} ----
+  const uint32_t t = threadIdx.x + (kA - kFirst);
+  if (threadIdx.x < kB - kA + 1) {
+    const uint32_t k = kA + threadIdx.x;
+    SegInfo& si = a.seg_info[k];
+    if (dense) {
+      si.E = kUndet;
+      si.Z = kUndet;
+      si.X = kUndet;  // forces the repair of this and the next segment
+      si.cnt = 0;
+      si.flags = kSegDense;
+    } else {
+      const uint64_t E = (k == 0) ? s0 : xs[t - 1];
+      const uint64_t sst = seg_start(a, s0, k);
+      const uint64_t e = seg_end(a, k);
+      LdsSrc src{cand, total, 0, lo};
+      src.seek(E);
+      uint64_t* out = a.stage + (uint64_t)k * a.scap;
+      uint32_t n = 0, flags = 0;
+      uint64_t x = E, last = E;
+      while (true) {
+        if (a.chain.is_last && x >= a.chain.L) { flags |= kSegEnd; break; }
+        const uint64_t nx = next_cut(x, src, a.chain);
+        if (nx == kUndet) { flags |= kSegUndet; break; }
+        if (nx > e) break;
+        if (nx > sst) {
+          if (n < a.scap) out[n] = nx;
+          ++n;
+        }
+        last = nx;
+        x = nx;
+      }
+      if (n > a.scap) flags |= kSegOverflow;
+      si.E = E;
+      si.Z = last;
+      si.cnt = n;
+      si.flags = flags;
+    }
+  }
+}
+
+// ---- K3: validity propagation, sequential repair, scan of counts ----------
+constexpr int kFixThreads = 1024;
+
+__device__ uint32_t bsearch_u64(const uint64_t* v, uint32_t n, uint64_t x) {
+  uint32_t l = 0, h = n;
+  while (l < h) {
+    const uint32_t m = (l + h) >> 1;
+    if (v[m] < x) l = m + 1; else h = m;
+  }
+  return l;
+}
+
+__global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
+  __shared__ uint32_t s_flag_cnt;
+  __shared__ uint64_t s_part[kFixThreads];
+  __shared__ int s_last_seg;
+  DevState* st = a.state;
+  if (st->done || *a.pc.overflow) {
+    if (threadIdx.x == 0) {
+      st->active = 0;
+      st->piece_cuts = 0;
+      if (*a.pc.overflow) st->err |= kErrDense;
+    }
+    return;
+  }
+  const uint32_t T = a.nseg;
+  const uint32_t kBad = kSegDense | kSegOverflow;
+
+  // (1) suspect segments: staged(k) was built from X_{k-1}; it is the true
+  //     chain iff staged(k-1) is and ended on X_{k-1} (Z_{k-1} == X_{k-1}).
+  if (threadIdx.x == 0) s_flag_cnt = 0;
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < T; k += kFixThreads) {
+    const SegInfo& si = a.seg_info[k];
+    bool bad = (si.flags & kBad) != 0;
+    if (k > 0) {
+      const SegInfo& sp = a.seg_info[k - 1];
+      bad = bad || (sp.X != sp.Z) || (sp.flags & kBad);
+    }
+    a.rep_cnt[k] = 0;
+    a.rep_from[k] = 0;
+    if (bad) a.flag_list[atomicAdd(&s_flag_cnt, 1u)] = k;
+  }
+  __syncthreads();
+  const uint32_t nflag = s_flag_cnt;
+
+  // (2) sequential repair, visiting only suspect segments and the segments a
+  //     repair runs into, until the true chain rejoins a staged chain.
+  if (nflag > 0 && threadIdx.x == 0) {
+    for (uint32_t i = 1; i < nflag; ++i) {  // insertion sort: the list is small
+      const uint32_t v = a.flag_list[i];
+      uint32_t j = i;
+      while (j > 0 && a.flag_list[j - 1] > v) { a.flag_list[j] = a.flag_list[j - 1]; --j; }
+      a.flag_list[j] = v;
+    }
+    GlobalSrc src{&a.pc};
+    const uint64_t s0 = st->carry;
+    uint32_t fi = 0, repaired = 0;
+    uint32_t k = a.flag_list[0];
+    bool rp = false;  // was segment k-1 repaired?
+    uint64_t rex = 0; // its repaired exit
+    while (k < T) {
+      const SegInfo& si = a.seg_info[k];
+      const uint64_t te = (k == 0) ? s0 : (rp ? rex : a.seg_info[k - 1].Z);
+      if ((si.flags & kBad) == 0 && si.E == te) {
+        // staged(k) entered from the true exit: valid; jump to next suspect
+        rp = false;
+        while (fi < nflag && a.flag_list[fi] <= k) ++fi;
+        if (fi >= nflag) break;
+        k = a.flag_list[fi];
+        continue;
+      }
+      // repair segment k from te until it lands on a staged cut
+      const uint64_t sst = (k == 0) ? s0 : a.anchor + (uint64_t)k * a.seg;
+      const uint64_t e = seg_end(a, k);
+      const uint64_t* stg = a.stage + (uint64_t)k * a.scap;
+      const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
+      uint64_t* rep = a.rep + (uint64_t)k * a.scap;
+      uint32_t n = 0;
+      uint64_t x = te, last = te;
+      bool joined = false;
+      while (true) {
+        if (a.chain.is_last && x >= a.chain.L) break;
+        const uint64_t nx = next_cut(x, src, a.chain);
+        if (nx == kUndet || nx > e) break;
+        if (nx > sst) {
+          const uint32_t idx = bsearch_u64(stg, scnt, nx);
+          if (idx < scnt && stg[idx] == nx) {
+            joined = true;
+            a.rep_from[k] = idx;
+            break;
+          }
+          if (n < a.scap) rep[n] = nx;
+          ++n;
+        }
+        last = nx;
+        x = nx;
+      }
+      if (n > a.scap) st->err |= kErrCapacity;
+      a.rep_cnt[k] = n;
+      if (!joined) a.rep_from[k] = scnt;
+      ++repaired;
+      rp = true;
+      rex = joined ? si.Z : last;
+      ++k;
+    }
+    st->repaired += repaired;
+  }
+  __syncthreads();
+
+  // (3) per-segment final counts -> exclusive scan -> output offsets
+  const uint32_t per = (T + kFixThreads - 1) / kFixThreads;
+  const uint32_t k0 = threadIdx.x * per < T ? threadIdx.x * per : T;
+  const uint32_t k1 = (k0 + per < T) ? k0 + per : T;
+  uint64_t mine = 0;
+  int last_nonempty = -1;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const SegInfo& si = a.seg_info[k];
+    const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
+    const uint64_t c = (uint64_t)a.rep_cnt[k] + (scnt - a.rep_from[k]);
+    mine += c;
+    if (c > 0) last_nonempty = (int)k;
+  }
+  s_part[threadIdx.x] = mine;
+  if (threadIdx.x == 0) s_last_seg = -1;
+  __syncthreads();
+  atomicMax(&s_last_seg, last_nonempty);
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (int i = 0; i < kFixThreads; ++i) {
+      const uint64_t v = s_part[i];
+      s_part[i] = acc;
+      acc += v;
+    }
+    st->piece_cuts = acc;
+  }
+  __syncthreads();
+  uint64_t off = st->total + s_part[threadIdx.x];
+  for (uint32_t k = k0; k < k1; ++k) {
+    const SegInfo& si = a.seg_info[k];
+    const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
+    a.out_off[k] = off;
+    off += (uint64_t)a.rep_cnt[k] + (scnt - a.rep_from[k]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int ls = s_last_seg;
+    if (ls >= 0) {
+      const SegInfo& si = a.seg_info[ls];
+      const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
+      uint64_t last;
+      if (scnt > a.rep_from[ls]) last = a.stage[(uint64_t)ls * a.scap + scnt - 1];
+      else last = a.rep[(uint64_t)ls * a.scap + a.rep_cnt[ls] - 1];
+      st->carry = last;
+    }
+    if (a.chain.is_last && st->carry >= a.chain.L) st->done = 1;
+    const uint64_t tot = st->total + st->piece_cuts;
+    if (tot > a.out_cap) st->err |= kErrCapacity;
+    st->total = tot;
+    st->active = 1;
+  }
+}
+
+// ---- K4: gather the per-segment lists into the contiguous output ---------
+__global__ __launch_bounds__(256) void gather_kernel(StitchArgs a) {
+  const uint32_t k = blockIdx.x;
+  if (k >= a.nseg) return;
+  if (!a.state->active || (a.state->err & kErrCapacity)) return;
+  const SegInfo& si = a.seg_info[k];
+  const uint32_t scnt = (si.flags & (kSegDense | kSegOverflow)) ? 0u : si.cnt;
+  const uint32_t rc = a.rep_cnt[k], rf = a.rep_from[k];
+  const uint64_t off = a.out_off[k];
+  const uint64_t* rep = a.rep + (uint64_t)k * a.scap;
+  const uint64_t* stg = a.stage + (uint64_t)k * a.scap;
+  for (uint32_t i = threadIdx.x; i < rc; i += blockDim.x) a.out[off + i] = rep[i];
+  for (uint32_t i = rf + threadIdx.x; i < scnt; i += blockDim.x) a.out[off + rc + (i - rf)] = stg[i];
+}
+
+}  // namespace dsx
+
+// ---- multi-GPU seam alignment (syncWith across ranks, make.go:277-298) ----
+#include "../../include/dsx.h"
+
+namespace dsx {
+
+struct SeamSrc {
+  const uint64_t* c;
+  uint32_t n;
+  uint32_t j;
+  __device__ uint64_t first_in(uint64_t a, uint64_t b) {
+    while (j < n && c[j] <= a) ++j;
+    if (j < n && c[j] <= b) return c[j];
+    return kNone;
+  }
+};
+
+// One lane walks the true chain across the seams in rank order: the chain
+// entering rank r (the exit of rank r-1's chain, true by induction) is walked
+// over rank r's seam window until it lands on a cut of rank r's speculative
+// chain (convergence c_r).  info: [0] 0 or 1+failing rank, [1] c_rank,
+// [2] number of cuts written to out (the true cuts of rank `rank` before c_r).
+__global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
+                                    uint64_t max, uint64_t* out, uint64_t* info) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  info[0] = 0;
+  info[1] = all[rank].shard_start;
+  info[2] = 0;
+  if (rank == 0) return;
+  uint64_t entry = all[0].exit_cut;
+  for (int r = 1; r <= rank && r < nranks; ++r) {
+    const dsx_seam_t& s = all[r];
+    ChainParams w;
+    w.min = min;
+    w.max = max;
+    w.L = s.total;
+    w.PE = s.window_end;
+    w.is_last = s.window_end == s.total ? 1u : 0u;
+    w.pad = 0;
+    SeamSrc src{s.cands, s.ncands, 0};
+    uint64_t x = entry, c = kNone;
+    uint32_t n = 0;
+    if (x == s.shard_start || s.shard_len == 0) {
+      c = s.shard_start;
+    } else {
+      while (true) {
+        if (w.is_last && x >= w.L) { c = x; break; }
+        const uint64_t nx = next_cut(x, src, w);
+        if (nx == kUndet) break;
+        const uint32_t idx = bsearch_u64(s.cuts, s.ncuts, nx);
+        if (idx < s.ncuts && s.cuts[idx] == nx) { c = nx; break; }
+        if (r == rank && n < DSX_SEAM_MAX_CUTS) out[n++] = nx;
+        x = nx;
+      }
+    }
+    if (c == kNone) {
+      info[0] = (uint64_t)r + 1;
+      return;
+    }
+    if (r == rank) {
+      info[1] = c;
+      info[2] = n;
+      return;
+    }
+    entry = s.shard_len == 0 ? entry : s.exit_cut;
+  }
+}
+
+}  // namespace dsx

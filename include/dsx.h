@@ -1,0 +1,202 @@
+/*
+ * dsx.h -- C ABI of the MI355X-native content-defined chunker (libdsx.so).
+ *
+ * Drop-in boundary for desync's chunking hot path.  Each entry point names the
+ * reference interface it replaces (paths relative to the desync repository):
+ *
+ *   dsx_params_init      <- NewChunker validation + constants, chunker.go:134-171
+ *                           (discriminatorFromAvg chunker.go:13-15, modInverse32
+ *                           chunker.go:20-28)
+ *   dsx_cut_device       <- the cut list IndexFromFile assembles, make.go:22-163,
+ *                           for a blob already resident in HBM
+ *   dsx_cut_host         <- IndexFromFile over an in-memory blob (pinned H2D
+ *                           pipeline inside the library)
+ *   dsx_cut_fd           <- IndexFromFile(ctx, name, ...) on an open file,
+ *                           make.go:49-116 (file read + H2D pipelined)
+ *   dsx_stream_*         <- Chunker.Next / Advance over an io.Reader,
+ *                           chunker.go:206-309 (stdin/pipe path, tar.go:140)
+ *   dsx_cancel           <- ctx cancellation -> Interrupted{}, make.go:201-203,
+ *                           errors.go:56-58
+ *   dsx_shard_*          <- make.go's split-and-align across GPUs: each rank
+ *                           chunks its range, then seams are aligned from a
+ *                           small all-gathered seam record (syncWith,
+ *                           make.go:277-327)
+ *
+ * Conventions (cgo-safe): plain pointers and sizes only; no pointer passed in
+ * is retained after a call returns; every function returns 0 or a negative
+ * DSX_E_* code; cut lists are chunk END offsets (the caibx table offsets,
+ * index.go:106-113), strictly increasing, the last one equal to the length.
+ * A context is not thread-safe (like a Chunker, one per goroutine/worker).
+ */
+#ifndef DSX_H
+#define DSX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSX_ABI_VERSION 1
+
+/* ---- error codes (negative) ---------------------------------------------- */
+enum {
+    DSX_OK = 0,
+    DSX_E_MIN_TOO_SMALL = -1,    /* "min chunk size too small, must be over 48"   chunker.go:135-137 */
+    DSX_E_MIN_GT_MAX = -2,       /* "min chunk size must not be greater than max"  chunker.go:138-140 */
+    DSX_E_MIN_GT_AVG = -3,       /* "min chunk size must not be greater than avg"  chunker.go:141-143 */
+    DSX_E_AVG_GT_MAX = -4,       /* "avg chunk size must not be greater than max"  chunker.go:144-146 */
+    DSX_E_AVG_RANGE = -5,        /* discriminatorFromAvg() <= 0 (Go: panic / implementation-defined) */
+    DSX_E_INVAL = -6,            /* bad argument (NULL pointer, bad flags) */
+    DSX_E_CAPACITY = -7,         /* output capacity too small; *n_out holds the required count */
+    DSX_E_HIP = -8,              /* HIP runtime error (see dsx_last_error) */
+    DSX_E_NOMEM = -9,            /* device or pinned allocation failed */
+    DSX_E_INTERRUPTED = -10,     /* dsx_cancel() was called: Interrupted{} errors.go:56-58 */
+    DSX_E_IO = -11,              /* read() on the file descriptor failed */
+    DSX_E_STATE = -12,           /* call not valid in the current stream state */
+    DSX_E_INTERNAL = -13         /* internal consistency check failed */
+};
+
+/* ---- chunker parameters ----------------------------------------------------
+ * Mirrors the Chunker fields of chunker.go:108-131.  Filled by
+ * dsx_params_init(); treat as opaque besides min/avg/max/discriminator. */
+typedef struct dsx_params {
+    uint64_t min, avg, max;
+    uint32_t discriminator; /* hDiscriminator */
+    uint32_t inverse_odd;   /* hInverseOdd */
+    uint32_t qmax;          /* hQMax */
+    uint32_t qbias;         /* hQBias */
+    int32_t rot;            /* k = trailing zeros of the discriminator (Go stores -k) */
+    uint32_t reserved;
+} dsx_params_t;
+
+/* NewChunker(r, min, avg, max) validation and constant derivation.
+ * Checks run in the order of chunker.go:135-146 and return the matching
+ * DSX_E_* code; dsx_strerror() returns the reference's exact message. */
+int dsx_params_init(uint64_t min, uint64_t avg, uint64_t max, dsx_params_t *out);
+const char *dsx_strerror(int code);
+int dsx_abi_version(void);
+
+/* ---- context ---------------------------------------------------------------- */
+typedef struct dsx_ctx dsx_ctx_t;
+
+/* Owns HIP streams, device scratch and pinned staging on `device`. */
+int dsx_ctx_create(int device, dsx_ctx_t **out);
+int dsx_ctx_destroy(dsx_ctx_t *ctx);
+/* Human-readable detail for the last DSX_E_HIP / DSX_E_INTERNAL on ctx
+ * (ctx == NULL: the reason the last dsx_ctx_create failed). */
+const char *dsx_last_error(dsx_ctx_t *ctx);
+/* Request cancellation of the running/next call; it returns DSX_E_INTERRUPTED. */
+int dsx_cancel(dsx_ctx_t *ctx);
+
+/* ---- one-shot cut lists ------------------------------------------------------ */
+#define DSX_OUT_HOST 0u   /* out_ends is host memory */
+#define DSX_OUT_DEVICE 1u /* out_ends is device memory on the ctx's device */
+#define DSX_NO_SYNC 2u    /* (device output only) enqueue on the ctx stream and return;
+                             fetch the count with dsx_result() (which waits) */
+
+/* Device-resident blob (HBM) -> cut list.  d_blob must stay valid until the
+ * call (or, with DSX_NO_SYNC, dsx_sync()) returns.  If cap is too small the
+ * call returns DSX_E_CAPACITY and *n_out holds the required count (an upper
+ * bound of len/min + 2 always suffices). */
+int dsx_cut_device(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, const dsx_params_t *p,
+                   uint64_t *out_ends, uint64_t cap, uint64_t *n_out, uint32_t flags);
+int dsx_sync(dsx_ctx_t *ctx);
+/* Completes a DSX_NO_SYNC dsx_cut_device(): waits, then returns its status and
+ * cut count (the device cut list is valid once this returns DSX_OK). */
+int dsx_result(dsx_ctx_t *ctx, uint64_t *n_out);
+
+/* Host-memory blob -> cut list (host).  Pipelined pinned H2D inside. */
+int dsx_cut_host(dsx_ctx_t *ctx, const void *h_blob, uint64_t len, const dsx_params_t *p,
+                 uint64_t *out_ends, uint64_t cap, uint64_t *n_out);
+
+/* File descriptor range [off, off+len) -> cut list (host).  len == UINT64_MAX
+ * means "until EOF".  The fd's file offset is not used or changed (pread). */
+int dsx_cut_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, const dsx_params_t *p,
+               uint64_t *out_ends, uint64_t cap, uint64_t *n_out);
+
+/* ---- streaming (Chunker.Next / Advance over an io.Reader) -------------------
+ * begin: resets the stream to position 0 with params p (NewChunker).
+ * push:  appends bytes read from the reader; eof=1 marks the end of input.
+ *        The library copies the bytes (caller keeps ownership).
+ * pop:   start and size of the next confirmed chunk.  Returns 1 if a chunk was
+ *        produced, 0 if more input is needed (or the stream ended: then
+ *        dsx_stream_done() is 1), or a negative error.
+ * advance: Chunker.Advance(n) (chunker.go:292-309): drop n bytes at the
+ *        current position (buffered first, then future pushes), reset the
+ *        hash state, and continue as if the stream started there.
+ * Chunk boundaries only depend on bytes in (start+min-48, start+max], so
+ * a chunk is confirmed as soon as those bytes have been pushed. */
+int dsx_stream_begin(dsx_ctx_t *ctx, const dsx_params_t *p);
+int dsx_stream_push(dsx_ctx_t *ctx, const void *bytes, uint64_t len, int eof);
+int dsx_stream_pop(dsx_ctx_t *ctx, uint64_t *start, uint64_t *size);
+int dsx_stream_advance(dsx_ctx_t *ctx, uint64_t n);
+int dsx_stream_done(dsx_ctx_t *ctx);
+/* Pointer to the bytes of the chunk returned by the last pop (host memory,
+ * valid until the next push/pop/advance -- Next()'s aliasing rule,
+ * chunker.go:202-205). */
+const uint8_t *dsx_stream_chunk_data(dsx_ctx_t *ctx);
+
+/* ---- multi-GPU shards (split-and-align across ranks) ------------------------
+ * A blob of total length `total` is range-sharded; rank r holds
+ * [shard_start, shard_start+shard_len) in device memory at d_shard, preceded
+ * by `halo` readable bytes (halo >= 48, or halo == 0 only when shard_start==0).
+ *
+ * dsx_shard_local: chunks the shard speculatively from a virtual cut at
+ *   shard_start (make.go's worker at span*i, make.go:94-116), keeps the
+ *   candidate positions of the first `seam_bytes` of the shard, and fills a
+ *   fixed-size seam record (dsx_seam_t) to be all-gathered between ranks.
+ * dsx_shard_resolve: given all ranks' seam records (rank order), aligns
+ *   every seam (syncWith, make.go:277-298) and returns this rank's final cut
+ *   list: the cuts c with shard_start < c <= shard_start+shard_len.
+ * Seam records are plain bytes; transport them with RCCL all-gather. */
+#define DSX_SEAM_MAX_CANDS 1024
+#define DSX_SEAM_MAX_CUTS 1024
+typedef struct dsx_seam {
+    uint64_t shard_start, shard_len, total;
+    uint64_t first_cand_beyond;   /* first candidate > window end, or UINT64_MAX */
+    uint64_t exit_cut;            /* speculative chain's last cut <= shard end */
+    uint64_t window_end;          /* candidates/cuts below cover (shard_start, window_end] */
+    uint32_t ncands, ncuts, flags, pad;
+    uint64_t cands[DSX_SEAM_MAX_CANDS]; /* candidate positions in (shard_start, window_end] */
+    uint64_t cuts[DSX_SEAM_MAX_CUTS];   /* spec chain cuts in (shard_start, window_end] */
+} dsx_seam_t;
+
+int dsx_shard_local(dsx_ctx_t *ctx, const void *d_shard, uint64_t halo, uint64_t shard_start,
+                    uint64_t shard_len, uint64_t total, const dsx_params_t *p, dsx_seam_t *seam);
+int dsx_shard_resolve(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, int rank,
+                      uint64_t *out_ends, uint64_t cap, uint64_t *n_out, uint32_t flags);
+
+/* ---- diagnostics ------------------------------------------------------------- */
+/* Evaluates the GPU boundary predicate (mode 0: multiply-inverse form of
+ * chunker.go:265, mode 1: float-reciprocal form, -1: the one the scan uses)
+ * for h in [h0, h0+n) (mod 2^32) against h % d == d-1 and counts mismatches
+ * (the check of chunker_test.go:190-213, on the device). */
+int dsx_selftest_boundary(dsx_ctx_t *ctx, const dsx_params_t *p, int mode, uint64_t h0,
+                          uint64_t n, uint64_t *mismatches);
+
+/* ---- synthetic inputs (bench / tests; generated on device) ------------------ */
+/* bytes [offset, offset+len) of the seeded uniform stream (splitmix64 of the
+ * 8-byte word index), written to d_dst. */
+int dsx_gen_uniform(dsx_ctx_t *ctx, void *d_dst, uint64_t offset, uint64_t len, uint64_t seed);
+/* dedup-realistic stream: 1 MiB blocks; block i is, with probability p_repeat,
+ * a copy of a uniformly chosen earlier block j < i, else fresh uniform bytes. */
+int dsx_gen_dedup(dsx_ctx_t *ctx, void *d_dst, uint64_t offset, uint64_t len, uint64_t seed,
+                  double p_repeat);
+
+/* ---- statistics (ChunkingStats, make.go:329-341 + scan/stitch timings) ------ */
+typedef struct dsx_stats {
+    uint64_t chunks;            /* ChunksAccepted */
+    uint64_t candidates;        /* boundary candidates found by the scan */
+    uint64_t pieces;            /* scan pieces processed */
+    uint64_t repaired_segments; /* segments that needed the sequential repair */
+    uint64_t dense_fallbacks;   /* pieces processed on the dense-candidate path */
+    float scan_ms, stitch_ms;   /* device time of the last call (HIP events) */
+} dsx_stats_t;
+int dsx_get_stats(dsx_ctx_t *ctx, dsx_stats_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSX_H */

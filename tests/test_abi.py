@@ -1,0 +1,68 @@
+"""C ABI checks that need no GPU: libdsx.so loads, exports every symbol that
+include/dsx.h declares, and NewChunker's validation matches chunker.go."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from desync_amd import _lib
+from oracle import oracle as o
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "dsx.h")
+
+
+def declared_functions():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(dsx_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    assert declared_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+
+
+def test_abi_version():
+    assert _lib.lib().dsx_abi_version() == 1
+
+
+@pytest.mark.parametrize("args,code,msg", [
+    ((47, 64, 128), _lib.DSX_E_MIN_TOO_SMALL, "min chunk size too small, must be over 48"),
+    ((200, 300, 100), _lib.DSX_E_MIN_GT_MAX, "min chunk size must not be greater than max"),
+    ((200, 100, 300), _lib.DSX_E_MIN_GT_AVG, "min chunk size must not be greater than avg"),
+    ((100, 300, 200), _lib.DSX_E_AVG_GT_MAX, "avg chunk size must not be greater than max"),
+])
+def test_param_validation_order_and_messages(args, code, msg):
+    p = _lib.Params()
+    assert _lib.lib().dsx_params_init(*args, ctypes.byref(p)) == code
+    assert _lib.lib().dsx_strerror(code).decode() == msg
+    with pytest.raises(ValueError, match=msg):
+        import desync_amd
+        desync_amd.Params(*args)
+
+
+def test_param_constants_match_oracle():
+    """dsx_params_init derives the same constants as chunker.go:147-170."""
+    avgs = [48, 64, 100, 1000, 4096, 8192, 16384, 65536, 100000, 262144, 1 << 20, 3 << 20,
+            8 << 20] + list(range(48, 5000, 37)) + list(range(60000, 70000, 113))
+    for avg in avgs:
+        p = _lib.Params()
+        assert _lib.lib().dsx_params_init(48, avg, avg, ctypes.byref(p)) == 0
+        P = o.params(48, avg, avg)
+        assert (p.discriminator, p.inverse_odd, p.qmax, p.qbias, p.rot) == \
+            (P.d, P.inv, P.qmax, P.qbias, P.rot), avg
+
+
+def test_no_gpu_context_fails_loudly():
+    """Without a GPU the context cannot be created -- there is no CPU path."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.DsxError):
+        _lib.Context(0)

@@ -1,0 +1,241 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle.
+
+Bit-exact for every cut.  Small inputs are compared cut-for-cut with the
+oracle; the reference's goldens (caibx files) are matched byte for byte end
+to end; at the BASELINE sizes the same comparison is made against the C
+oracle on the same seeded bytes (regenerated on the CPU).
+"""
+import ctypes
+import io
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as o
+
+pytestmark = pytest.mark.gpu
+
+MIN, AVG, MAX = 16 * 1024, 64 * 1024, 256 * 1024
+
+
+def torch_dev(arr):
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.uint8)).to("cuda")
+    torch.cuda.synchronize()
+    return t
+
+
+def gpu_cut(dctx, arr, mn=MIN, av=AVG, mx=MAX):
+    import desync_amd
+    t = torch_dev(arr)
+    return desync_amd.cut_device(t.data_ptr(), t.numel(), mn, av, mx, ctx=dctx)
+
+
+# ---------------------------------------------------------------- predicate
+@pytest.mark.parametrize("avg", [16 * 1024, 64 * 1024, 256 * 1024, 1024 * 1024, 8192, 4096, 1000])
+@pytest.mark.parametrize("mode", [0, 1, -1])
+def test_boundary_predicate_ranges(dctx, avg, mode):
+    """chunker_test.go:190-213 on the device: [0,3d) and [2^32-1-3d, 2^32)."""
+    import desync_amd
+    from desync_amd import _lib
+    p = desync_amd.Params(max(48, avg // 4), avg, avg * 4)
+    d = p.discriminator
+    if mode == 1 and not (2048 < d < (1 << 24)):
+        pytest.skip("float form is only used for 2048 < d < 2^24")
+    for h0, n in ((0, 3 * d), (2**32 - 1 - 3 * d, 3 * d + 1)):
+        bad = ctypes.c_uint64()
+        _lib.check(_lib.lib().dsx_selftest_boundary(dctx.h, ctypes.byref(p.c), mode, h0, n,
+                                                    ctypes.byref(bad)), dctx.h)
+        assert bad.value == 0
+
+
+@pytest.mark.parametrize("avg", [16 * 1024, 64 * 1024, 256 * 1024])
+def test_boundary_predicate_exhaustive(dctx, avg):
+    """All 2^32 hash values for the BASELINE discriminators."""
+    import desync_amd
+    from desync_amd import _lib
+    p = desync_amd.Params(avg // 4, avg, avg * 4)
+    bad = ctypes.c_uint64()
+    _lib.check(_lib.lib().dsx_selftest_boundary(dctx.h, ctypes.byref(p.c), -1, 0, 1 << 32,
+                                                ctypes.byref(bad)), dctx.h)
+    assert bad.value == 0
+
+
+# ---------------------------------------------------------------- goldens
+GOLDEN_PAIRS = [
+    ("chunker.input", "chunker.index"),
+    ("blob1", "blob1.caibx"),
+    ("blob2", "blob2.caibx"),
+    ("tree.catar", "tree.caidx"),
+]
+
+
+@pytest.mark.parametrize("inp,idx", GOLDEN_PAIRS)
+def test_device_cuts_match_golden(dctx, golden, inp, idx):
+    data = np.frombuffer(golden(inp), np.uint8)
+    d = o.decode_caibx(golden(idx))
+    ends = gpu_cut(dctx, data, d["min"], d["avg"], d["max"])
+    assert np.array_equal(ends, d["ends"])
+
+
+@pytest.mark.parametrize("inp,idx", GOLDEN_PAIRS)
+def test_index_from_file_bit_identical(dctx, golden, inp, idx, tmp_path):
+    """desync make: IndexFromFile + WriteTo == the reference's caibx bytes."""
+    import desync_amd
+    ref = golden(idx)
+    d = o.decode_caibx(ref)
+    f = tmp_path / inp
+    f.write_bytes(golden(inp))
+    index, stats = desync_amd.IndexFromFile(None, str(f), 4, d["min"], d["avg"], d["max"])
+    b = io.BytesIO()
+    index.WriteTo(b)
+    assert b.getvalue() == ref
+    assert stats.ChunksAccepted == len(d["ends"])
+
+
+def test_large_file_next(dctx, golden):
+    """TestChunkerLargeFile through Chunker.Next (streaming path)."""
+    import desync_amd
+    from test_oracle_golden import LARGE_FILE
+    import hashlib
+    c = desync_amd.NewChunker(io.BytesIO(golden("chunker.input")), MIN, AVG, MAX, ctx=dctx)
+    for start, size, sid in LARGE_FILE:
+        s, b = c.Next()
+        assert (s, len(b), hashlib.new("sha512_256", b).hexdigest()) == (start, size, sid)
+    s, b = c.Next()
+    assert b == b""
+
+
+# ---------------------------------------------------------------- edge cases
+def test_edge_cases(dctx):
+    """chunker_test.go:69-131 on the device path."""
+    import desync_amd
+    import torch
+    t = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    assert desync_amd.cut_device(t.data_ptr(), 0, MIN, AVG, MAX, ctx=dctx).size == 0
+    assert gpu_cut(dctx, np.arange(16, dtype=np.uint8)).tolist() == [16]
+    assert gpu_cut(dctx, np.zeros(1 << 20, np.uint8)).tolist() == [MAX * (i + 1) for i in range(4)]
+    for size in (MIN, AVG, MAX):
+        assert gpu_cut(dctx, np.zeros(size, np.uint8)).tolist() == [size]
+    for size in (1, 47, 48, 49, MIN - 1, MIN + 1, MIN + 48, MIN + 49, MAX + 1, 2 * MAX - 1):
+        data = o.synth_uniform(11, 0, size)
+        assert np.array_equal(gpu_cut(dctx, data), o.chunk_stream(data, MIN, AVG, MAX)), size
+
+
+def test_chunker_advance(dctx):
+    """TestChunkerAdvance (chunker_test.go:134-175)."""
+    import desync_amd
+    null = bytes(MAX)
+    data_a = b"a" * 128
+    data_b = b"b" * (12 * MAX)
+    inp = null + data_a + null + data_b
+    c = desync_amd.NewChunker(io.BytesIO(inp), MIN, AVG, MAX, ctx=dctx)
+    _, b = c.Next()
+    assert b == null
+    c.Advance(len(data_a))
+    _, b = c.Next()
+    assert b == null
+    c.Advance(len(data_b))
+    _, b = c.Next()
+    assert b == b""
+
+
+# ---------------------------------------------------------------- seeded random
+@pytest.mark.parametrize("seed,size", [(1, 1 << 20), (2, 3 * (1 << 20) + 12345), (3, 17 << 20),
+                                       (4, 64 << 20)])
+def test_random_default_params(dctx, seed, size):
+    data = o.synth_uniform(seed, 0, size)
+    assert np.array_equal(gpu_cut(dctx, data), o.chunk_stream(data, MIN, AVG, MAX))
+
+
+@pytest.mark.parametrize("avg", [16 * 1024, 64 * 1024, 256 * 1024, 8192, 4096, 2048, 1000, 192])
+def test_random_avg_sweep(dctx, avg):
+    mn, mx = max(48, avg // 4), avg * 4
+    data = o.synth_uniform(5, 0, 9 << 20)
+    assert np.array_equal(gpu_cut(dctx, data, mn, avg, mx), o.chunk_stream(data, mn, avg, mx))
+
+
+def test_odd_params(dctx):
+    """min == avg == max, min = 48, max >> avg."""
+    data = o.synth_uniform(6, 0, 3 << 20)
+    for mn, av, mx in ((48, 48, 48), (48, 4096, 1 << 20), (1000, 1000, 1000), (4096, 4096, 65536),
+                       (64, 100, 50000)):
+        assert np.array_equal(gpu_cut(dctx, data, mn, av, mx), o.chunk_stream(data, mn, av, mx)), \
+            (mn, av, mx)
+
+
+def test_null_compositions(dctx):
+    """make_test.go:16-80 inputs (random/null blocks of 4*max)."""
+    rng = np.random.default_rng(7)
+    null = np.zeros(4 * MAX, np.uint8)
+    r1 = rng.integers(0, 256, 4 * MAX, dtype=np.uint8)
+    r2 = rng.integers(0, 256, 4 * MAX, dtype=np.uint8)
+    for parts in ([r1, r2, r1, r2, r1], [null] * 4 + [r1, r2], [r1, r2] + [null] * 4,
+                  [r1] + [null] * 4 + [r2], [r1, null, null, null, r1, null, null, null, r2]):
+        data = np.concatenate(parts)
+        assert np.array_equal(gpu_cut(dctx, data), o.chunk_stream(data, MIN, AVG, MAX))
+
+
+def test_periodic_dense_candidates(dctx):
+    """Adversarial data with a boundary candidate every 48 bytes: chains never
+    re-synchronise, exercising the dense-slot path and the sequential repair."""
+    P = o.params(MIN, AVG, MAX)
+    rng = np.random.default_rng(1)
+    while True:  # find a 48-byte block whose periodic window hash is a candidate
+        blk = rng.integers(0, 256, 48, dtype=np.uint8)
+        if o.window_hash(bytes(blk)) % P.d == P.d - 1:
+            break
+    data = np.tile(blk, (3 << 20) // 48)
+    assert np.array_equal(gpu_cut(dctx, data), o.chunk_stream(data, MIN, AVG, MAX))
+
+
+# ---------------------------------------------------------------- host paths
+def test_host_and_fd_paths(dctx, tmp_path):
+    import desync_amd
+    data = o.synth_uniform(8, 0, (600 << 20) + 777)  # > one 256 MiB pipeline chunk
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    assert np.array_equal(desync_amd.cut_host(data, MIN, AVG, MAX, ctx=dctx), ref)
+    f = tmp_path / "blob"
+    data.tofile(str(f))
+    fd = os.open(str(f), os.O_RDONLY)
+    try:
+        assert np.array_equal(desync_amd.cut_fd(fd, MIN, AVG, MAX, ctx=dctx), ref)
+    finally:
+        os.close(fd)
+
+
+def test_stream_matches(dctx):
+    import desync_amd
+    data = o.synth_uniform(9, 0, (40 << 20) + 5)
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    c = desync_amd.NewChunker(io.BytesIO(data.tobytes()), MIN, AVG, MAX, ctx=dctx)
+    ends = [s + len(b) for s, b in c]
+    assert ends == ref.tolist()
+
+
+# ---------------------------------------------------------------- BASELINE sizes
+def test_config2_1gib_uniform(dctx):
+    """BASELINE config 2: 1 GiB uniform bytes (seed 1), default params + sweep."""
+    import desync_amd
+    import torch
+    n = 1 << 30
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    from desync_amd import _lib
+    _lib.check(_lib.lib().dsx_gen_uniform(dctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 1), dctx.h)
+    host = t.cpu().numpy()
+    assert np.array_equal(host[:4096], o.synth_uniform(1, 0, 4096))
+    for mn, av, mx in ((MIN, AVG, MAX), (4096, 16384, 65536), (65536, 262144, 1 << 20)):
+        got = desync_amd.cut_device(t.data_ptr(), n, mn, av, mx, ctx=dctx)
+        assert np.array_equal(got, o.chunk_stream(host, mn, av, mx)), (mn, av, mx)
+
+
+def test_config4_zeros(dctx):
+    """BASELINE config 4 (scaled to 4 GiB here): forced max-size chunks only."""
+    import desync_amd
+    import torch
+    n = 4 << 30
+    t = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    got = desync_amd.cut_device(t.data_ptr(), n, MIN, AVG, MAX, ctx=dctx)
+    assert got.size == n // MAX
+    assert np.array_equal(got, np.arange(1, n // MAX + 1, dtype=np.uint64) * MAX)
