@@ -25,7 +25,7 @@
 #include "dsx_stitch.h"
 
 namespace dsx {
-template <int MODE>
+template <int MODE, int VARIANT, int BR, int NBUF>
 __global__ void scan_kernel(ScanArgs a);
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
@@ -50,7 +50,8 @@ constexpr uint64_t kPieceMax = 8ull << 30;       // bytes per scan launch
 constexpr uint64_t kHostChunk = 256ull << 20;    // host-resident pipeline chunk
 constexpr uint64_t kStreamBatch = 16ull << 20;   // streaming: bytes per device batch
 constexpr uint32_t kWalkLdsCap = 12288;          // candidates per walk workgroup
-constexpr uint32_t kDenseS = 480;                // dense path lane bytes (= slot cap)
+constexpr uint32_t kDenseS = 48 * 11;            // dense path lane bytes (= slot cap), BR=4
+constexpr uint32_t kDenseS2 = 48 * 9;            // dense path lane bytes, BR=2
 constexpr uint64_t kDensePiece = 32ull << 20;    // dense path piece size
 
 template <class T>
@@ -85,8 +86,11 @@ struct dsx_ctx {
   std::atomic<int> cancel{0};
   std::string err;
   int force_mode = -1;  // DSX_TEST_MODE env override
+  int variant = 0;      // DSX_SCAN_VARIANT: diagnostic scan ablations (wrong results)
+  uint32_t lane_bytes_override = 0;  // DSX_LANE_BYTES (tuning; multiple of 48)
+  int batch_rounds = 4;               // DSX_BATCH_ROUNDS: scan staging (4x1 or 2x2)
 
-  DevBuf<uint32_t> lane_cnt, overflow, rep_cnt, rep_from, flag_list;
+  DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
   DevBuf<uint16_t> lane_slot;
   DevBuf<SegInfo> seg_info;
   DevBuf<uint64_t> stage, rep, out_off, out;
@@ -94,7 +98,10 @@ struct dsx_ctx {
   DevBuf<uint8_t> dbuf[2];
   uint8_t* pinned[2] = {nullptr, nullptr};
   size_t pinned_sz = 0;
-  DevState* h_state = nullptr;  // pinned mirror
+  HostState* h_state = nullptr;  // pinned mirror published by fixup_kernel
+  uint64_t piece_seq = 0;        // global piece counter (overflow parity, freshness)
+  bool init_pending = false;     // next scan initialises DevState with init_carry
+  uint64_t init_carry = 0;
 
   // streaming state (Chunker.Next over an io.Reader)
   struct Stream {
@@ -222,14 +229,19 @@ static TestConsts make_tc(const dsx_params_t* p) {
   tc.qbias = p->qbias;
   tc.rot = (uint32_t)p->rot;
   tc.rcp = 1.0f / (float)p->discriminator;
-  tc.c0 = (float)(0.5 - (double)(p->discriminator - 1u) / (double)p->discriminator);
+  // MODE 1 (is_cand in dsx_scan.hip): fma(h, 1/d, 1.5*2^23 - 1) puts
+  // round(h/d) - 1 + 0x400000 in the low mantissa bits; madc folds the
+  // 0x400000*d offset and the -1 back into the exact 24-bit check.
+  tc.c0 = 12582911.0f;
+  tc.madc = p->discriminator - 1u - (p->discriminator << 22);
+  tc.pad = 0;
   return tc;
 }
 
-// float-reciprocal test is exact for 2048 < d < 2^24 (DESIGN.md "Boundary test")
+// float magic-number test is exact for 1024 < d < 2^22 (DESIGN.md "Boundary test")
 static int pick_mode(const dsx_ctx* c, uint32_t d) {
   if (c->force_mode == 0 || c->force_mode == 1) return c->force_mode;
-  return (d > 2048u && d < (1u << 24)) ? 1 : 0;
+  return (d > 1024u && d < (1u << 22)) ? 1 : 0;
 }
 
 // --------------------------------------------------------------------------
@@ -258,6 +270,12 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   CREATE_STEP(hipGetDeviceProperties(&prop, device));
   c->ncu = prop.multiProcessorCount;
   if (const char* m = getenv("DSX_TEST_MODE")) c->force_mode = atoi(m);
+  if (const char* v = getenv("DSX_SCAN_VARIANT")) c->variant = atoi(v);
+  if (const char* v = getenv("DSX_BATCH_ROUNDS")) c->batch_rounds = atoi(v) == 2 ? 2 : 4;
+  if (const char* v = getenv("DSX_LANE_BYTES")) {
+    const long lb = atol(v);
+    if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
+  }
   CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   CREATE_STEP(hipEventCreate(&c->ev_t0));
@@ -267,9 +285,12 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     CREATE_STEP(hipEventCreateWithFlags(&c->copy_done[i], hipEventDisableTiming));
     CREATE_STEP(hipEventCreateWithFlags(&c->comp_done[i], hipEventDisableTiming));
   }
-  CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(DevState)));
+  CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
+  memset(c->h_state, 0, sizeof(HostState));
   CREATE_STEP(c->state.ensure(1));
-  CREATE_STEP(c->overflow.ensure(1));
+  CREATE_STEP(c->overflow.ensure(2));
+  CREATE_STEP(hipMemset(c->overflow.p, 0, 2 * sizeof(uint32_t)));
+  CREATE_STEP(hipMemset(c->state.p, 0, sizeof(DevState)));
 #undef CREATE_STEP
   *out = c;
   return DSX_OK;
@@ -280,7 +301,7 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
-  c->lane_cnt.release(); c->overflow.release(); c->rep_cnt.release(); c->rep_from.release();
+  c->region_cnt.release(); c->region_list.release(); c->overflow.release(); c->rep_cnt.release(); c->rep_from.release();
   c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
   c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
   c->dbuf[0].release(); c->dbuf[1].release();
@@ -324,21 +345,23 @@ struct CallCfg {
   uint64_t halo0 = 0;  // readable bytes before the first piece (shards)
 };
 
+// The next scan launch initialises the device chain state (no memcpy).
 static int reset_state(dsx_ctx* c, uint64_t carry) {
   c->npiece_call = 0;
-  DevState s{};
-  s.carry = carry;
-  *c->h_state = s;
-  HIPCHK(c, hipMemcpyAsync(c->state.p, c->h_state, sizeof(DevState), hipMemcpyHostToDevice,
-                           c->stream));
+  c->init_pending = true;
+  c->init_carry = carry;
   return DSX_OK;
 }
 
-static int read_state(dsx_ctx* c, DevState* out) {
-  HIPCHK(c, hipMemcpyAsync(c->h_state, c->state.p, sizeof(DevState), hipMemcpyDeviceToHost,
-                           c->stream));
+// Wait for the stream; the last fixup_kernel published the state into pinned
+// host memory.
+static int read_state(dsx_ctx* c, HostState* out) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  *out = *c->h_state;
+  memcpy(out, (const void*)c->h_state, sizeof(HostState));
+  if (out->seq != c->piece_seq) {
+    c->err = "stale chain state (no piece completed)";
+    return DSX_E_INTERNAL;
+  }
   return DSX_OK;
 }
 
@@ -348,27 +371,43 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
                          uint64_t P, uint64_t len, bool is_last) {
   const dsx_params_t* p = cc.p;
   // ---- scan geometry: balance regions over the persistent grid ----
+  // lane segment S = 48*(4k-1): the warm-up round plus S/48 rounds fill k
+  // whole 4-round DMA batches
   const uint64_t slots_total = (uint64_t)c->ncu * kScanWaves;  // wave slots
   uint32_t S, LS;
   if (cc.dense) {
-    S = kDenseS;
-    LS = kDenseS;
+    S = c->batch_rounds == 4 ? kDenseS : kDenseS2;
+    LS = S;
   } else {
     const uint64_t per_lane = (len + slots_total * 64 - 1) / (slots_total * 64);
-    const uint64_t k = (per_lane + kMaxLaneBytes - 1) / kMaxLaneBytes;  // region rounds
-    uint64_t s = (len + k * slots_total * 64 - 1) / (k * slots_total * 64);
-    s = (s + kRound - 1) / kRound * kRound;
-    if (s < 48u * 16u) s = 48u * 16u;
-    if (s > kMaxLaneBytes) s = kMaxLaneBytes;
+    const uint64_t rounds_needed = (per_lane + kMaxLaneBytes - 1) / kMaxLaneBytes;  // waves/slot
+    uint64_t s = (len + rounds_needed * slots_total * 64 - 1) / (rounds_needed * slots_total * 64);
+    const uint64_t BR = (uint64_t)c->batch_rounds;
+    uint64_t kb = (s / kRound + 1 + BR - 1) / BR;  // batches
+    if (kb < 4) kb = 4;
+    while (kRound * (BR * kb - 1) > kMaxLaneBytes) --kb;
+    s = (uint64_t)kRound * (BR * kb - 1);
+    if (c->lane_bytes_override && (c->lane_bytes_override / kRound + 1) % BR == 0)
+      s = c->lane_bytes_override;
     S = (uint32_t)s;
     LS = kLaneSlots;
   }
+  const uint32_t batches = (S / kRound + 1) / (uint32_t)c->batch_rounds;
   const uint64_t region_bytes = 64ull * S;
   const uint64_t nregions = len == 0 ? 0 : (len + region_bytes - 1) / region_bytes;
   const uint64_t nlanes = nregions * 64;
-  HIPCHK(c, grow(c, c->lane_cnt, nlanes));
+  uint32_t rcap;
+  if (cc.dense) {
+    rcap = 64u * S;
+  } else {
+    const double expct = (double)region_bytes / (double)p->discriminator;
+    rcap = (uint32_t)std::min<double>(64.0 * S, 4.0 * expct + 64.0);
+    rcap = (rcap + 63u) & ~63u;
+  }
   HIPCHK(c, grow(c, c->lane_slot, nlanes * LS));
-  HIPCHK(c, hipMemsetAsync(c->overflow.p, 0, sizeof(uint32_t), c->stream));
+  HIPCHK(c, grow(c, c->region_cnt, nregions));
+  HIPCHK(c, grow(c, c->region_list, nregions * rcap));
+  const uint64_t seq = ++c->piece_seq;
 
   ScanArgs sa{};
   sa.base = d_piece;
@@ -376,14 +415,20 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   sa.piece_abs = P;
   sa.len = len;
   sa.lane_bytes = S;
-  sa.rounds = S / kRound;
+  sa.batches = batches;
   sa.nregions = (uint32_t)nregions;
+  sa.region_cap = rcap;
   sa.tc = make_tc(p);
   sa.min_pos = cc.min_pos;
   sa.lane_slots = LS;
-  sa.lane_cnt = c->lane_cnt.p;
   sa.lane_slot = c->lane_slot.p;
-  sa.overflow = c->overflow.p;
+  sa.region_cnt = c->region_cnt.p;
+  sa.region_list = c->region_list.p;
+  sa.overflow = c->overflow.p + (seq & 1);
+  sa.overflow_next = c->overflow.p + ((seq + 1) & 1);
+  sa.state_init = c->init_pending ? (void*)c->state.p : nullptr;
+  sa.init_carry = c->init_carry;
+  c->init_pending = false;
   const uint32_t pi = c->npiece_call++;
   while (c->pev.size() < 3 * (size_t)(pi + 1)) {
     hipEvent_t e;
@@ -391,16 +436,29 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     c->pev.push_back(e);
   }
   HIPCHK(c, hipEventRecord(c->pev[3 * pi], c->stream));
-  if (nregions > 0) {
-    const uint64_t need_wg = (nregions + kScanWaves - 1) / kScanWaves;
+  {
+    const uint64_t need_wg = std::max<uint64_t>(1, (nregions + kScanWaves - 1) / kScanWaves);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)c->ncu);
-    if (pick_mode(c, p->discriminator) == 1)
-      hipLaunchKernelGGL(scan_kernel<1>, dim3(grid), dim3(kScanThreads), 0, c->stream, sa);
+    const dim3 g(grid), b(kScanThreads);
+    const int mode = pick_mode(c, p->discriminator);
+#define DSX_LAUNCH(BR, NB)                                                              \
+  do {                                                                                  \
+    if (c->variant == 1)                                                                \
+      hipLaunchKernelGGL((scan_kernel<1, 1, BR, NB>), g, b, 0, c->stream, sa);          \
+    else if (c->variant == 3)                                                           \
+      hipLaunchKernelGGL((scan_kernel<1, 3, BR, NB>), g, b, 0, c->stream, sa);          \
+    else if (mode == 1)                                                                 \
+      hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB>), g, b, 0, c->stream, sa);          \
+    else                                                                                \
+      hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB>), g, b, 0, c->stream, sa);          \
+  } while (0)
+    if (c->batch_rounds == 4)
+      DSX_LAUNCH(4, 1);
     else
-      hipLaunchKernelGGL(scan_kernel<0>, dim3(grid), dim3(kScanThreads), 0, c->stream, sa);
+      DSX_LAUNCH(2, 2);
+#undef DSX_LAUNCH
     HIPCHK(c, hipGetLastError());
   }
-
   HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));
   // ---- stitch geometry ----
   StitchArgs ta{};
@@ -410,12 +468,12 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.chain.PE = P + len;
   ta.chain.is_last = is_last ? 1u : 0u;
   ta.pc.P = P;
-  ta.pc.nlanes = nlanes;
-  ta.pc.S = S;
-  ta.pc.lane_slots = LS;
-  ta.pc.lane_cnt = c->lane_cnt.p;
-  ta.pc.lane_slot = c->lane_slot.p;
-  ta.pc.overflow = c->overflow.p;
+  ta.pc.RB = region_bytes;
+  ta.pc.nregions = (uint32_t)nregions;
+  ta.pc.region_cap = rcap;
+  ta.pc.region_cnt = c->region_cnt.p;
+  ta.pc.region_list = c->region_list.p;
+  ta.pc.overflow = sa.overflow;
   // the carried cut lies in (P - max, P] (its successor needed bytes >= P)
   const uint64_t anchor = (P > cc.origin + p->max) ? P - p->max : cc.origin;
   const uint64_t seg = std::max<uint64_t>(8 * p->max, 1ull << 20);
@@ -426,6 +484,10 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.nseg = (uint32_t)nseg;
   const double exp_per_seg = (double)seg / (double)p->discriminator + 8.0;
   uint64_t spg = (uint64_t)((double)kWalkLdsCap / (2.0 * exp_per_seg)) - 1;
+  // the WG's regions (spg+1 segments) must fit one region per thread
+  const uint64_t max_spg_reg = region_bytes ? (200ull * region_bytes) / seg : kMaxSpg;
+  spg = std::min<uint64_t>(spg, max_spg_reg > 2 ? max_spg_reg - 2 : 1);
+  spg = std::min<uint64_t>(spg, 32);  // parallelism: >= T/32 walk workgroups
   spg = std::max<uint64_t>(1, std::min<uint64_t>(spg, kMaxSpg));
   ta.spg = (uint32_t)spg;
   ta.lds_cap = kWalkLdsCap;
@@ -447,6 +509,8 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.out = cc.d_out;
   ta.out_cap = cc.out_cap;
   ta.state = c->state.p;
+  ta.host_state = c->h_state;
+  ta.seq = seq;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
   const size_t walk_lds = (size_t)kWalkLdsCap * 4 + (kMaxSpg + 1) * 8;
   hipLaunchKernelGGL(walk_kernel, dim3(walk_grid), dim3(256), walk_lds, c->stream, ta);
@@ -487,7 +551,7 @@ static int ensure_attr_walk(dsx_ctx* c) {
 }
 
 static int finish_call(dsx_ctx* c, uint64_t* n_out, uint64_t cap, bool* dense_retry) {
-  DevState s;
+  HostState s;
   int rc = read_state(c, &s);
   if (rc) return rc;
   *dense_retry = false;
@@ -755,7 +819,7 @@ static int stream_process(dsx_ctx* c) {
         if (rc) return rc;
       }
     }
-    DevState st;
+    HostState st;
     rc = read_state(c, &st);
     if (rc) return rc;
     if (st.err & kErrDense) {
@@ -954,7 +1018,7 @@ extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
       if (rc) return rc;
     }
     HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
-    DevState st;
+    HostState st;
     rc = read_state(c, &st);
     if (rc) return rc;
     if (st.err & kErrDense) {
@@ -984,15 +1048,17 @@ extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
                          is_last && wlen == shard_len);
       if (rc) return rc;
       HIPCHK(c, hipStreamSynchronize(c->stream));
-      // read back lane lists of the dense-path scan of the window
-      const uint64_t S = kDenseS;
-      const uint64_t nl = (wlen + 64 * S - 1) / (64 * S) * 64;
-      std::vector<uint32_t> cnt(nl);
-      std::vector<uint16_t> sl(nl * S);
-      HIPCHK(c, hipMemcpy(cnt.data(), c->lane_cnt.p, nl * 4, hipMemcpyDeviceToHost));
-      HIPCHK(c, hipMemcpy(sl.data(), c->lane_slot.p, nl * S * 2, hipMemcpyDeviceToHost));
-      for (uint64_t g = 0; g < nl; ++g)
-        for (uint32_t i = 0; i < cnt[g] && i < S; ++i) cands.push_back(shard_start + g * S + sl[g * S + i]);
+      // read back the region lists of the dense-path scan of the window
+      const uint64_t RB = 64ull * (c->batch_rounds == 4 ? kDenseS : kDenseS2);
+      const uint64_t nr = (wlen + RB - 1) / RB;
+      const uint64_t cap = RB;  // dense path: region_cap == region bytes
+      std::vector<uint32_t> cnt(nr);
+      std::vector<uint32_t> lst(nr * cap);
+      HIPCHK(c, hipMemcpy(cnt.data(), c->region_cnt.p, nr * 4, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(lst.data(), c->region_list.p, nr * cap * 4, hipMemcpyDeviceToHost));
+      for (uint64_t r = 0; r < nr; ++r)
+        for (uint32_t i = 0; i < cnt[r] && i < cap; ++i)
+          cands.push_back(shard_start + r * RB + lst[r * cap + i]);
     }
     if (cands.size() > DSX_SEAM_MAX_CANDS) {
       seam->first_cand_beyond = cands[DSX_SEAM_MAX_CANDS];

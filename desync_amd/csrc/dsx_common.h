@@ -18,12 +18,13 @@ constexpr int kWave = 64;
 constexpr int kScanWaves = 8;                 // waves per workgroup (2 per SIMD)
 constexpr int kScanThreads = kScanWaves * kWave;
 constexpr int kRound = 48;                    // bytes per lane per round == window
-constexpr int kNBuf = 4;                      // LDS staging ring depth per wave
-constexpr int kStageBytes = kWave * kRound;   // 3072 B per staging buffer
+constexpr int kStageBytesPerWave = 12288;     // LDS-DMA staging per wave (BR*NBUF*48*64)
 constexpr int kTableBytes = 256 * 256;        // 256 byte values x 32 lane slots x {T,Trot}
-constexpr int kScanLds = kTableBytes + kScanWaves * kNBuf * kStageBytes;  // 163840
+constexpr int kScanLds = kTableBytes + kScanWaves * kStageBytesPerWave;  // 163840
 constexpr int kLaneSlots = 32;                // candidate slots per lane segment
-constexpr uint32_t kMaxLaneBytes = 48u * 1365u;  // keeps slot offsets in u16
+// lane segment = 48*(BR*k-1) bytes (warm-up round + segment = whole batches);
+// offsets stay in u16
+constexpr uint32_t kMaxLaneBytes = 48u * (4u * 341u - 1u);  // 65424
 
 static_assert(kScanLds <= 163840, "scan LDS budget exceeds 160 KiB");
 
@@ -31,6 +32,8 @@ static_assert(kScanLds <= 163840, "scan LDS budget exceeds 160 KiB");
 struct TestConsts {
   uint32_t d;      // discriminator
   uint32_t dm1;    // d - 1
+  uint32_t madc;   // MODE 1: d - 1 - (d << 22) (folds the float offset, see is_cand)
+  uint32_t pad;
   uint32_t inv;    // inverse of odd part of d mod 2^32
   uint32_t qmax;   // (2^32-1)/d - qbias
   uint32_t qbias;
@@ -44,17 +47,21 @@ struct ScanArgs {
   uint64_t halo;         // readable bytes before base (0 only at blob start)
   uint64_t piece_abs;    // absolute blob position of base[0]
   uint64_t len;          // piece length in bytes
-  uint32_t lane_bytes;   // S, multiple of kRound
-  uint32_t rounds;       // S / kRound
+  uint32_t lane_bytes;   // S = 48*(BR*batches - 1)
+  uint32_t batches;      // (S/48 + 1) / BR
   uint32_t nregions;     // ceil(len / (64*S))
-  uint32_t pad;
+  uint32_t region_cap;   // list capacity per region
   TestConsts tc;
   uint64_t min_pos;      // candidates at absolute p < min_pos are dropped (origin + 49)
   uint32_t lane_slots;   // slot capacity per lane (kLaneSlots, or S on the dense path)
   uint32_t pad2;
-  uint32_t* lane_cnt;    // [nregions*64] candidates per lane segment (exact)
-  uint16_t* lane_slot;   // [nregions*64*lane_slots] offsets o in [1,S] (p = lane base + o)
-  uint32_t* overflow;    // number of lane segments with more than kLaneSlots
+  uint16_t* lane_slot;   // scratch [nregions*64*lane_slots]: per-lane hits (rare writes)
+  uint32_t* region_cnt;  // [nregions] candidates per region (exact)
+  uint32_t* region_list; // [nregions*region_cap] sorted offsets in (0, 64*S] from region base
+  uint32_t* overflow;    // regions whose lanes or list overflowed (-> dense path)
+  uint32_t* overflow_next;  // the next piece's counter: zeroed here (parity buffers)
+  void* state_init;      // if non-null: DevState to initialise (first piece of a call)
+  uint64_t init_carry;
 };
 
 // Sentinel for "successor depends on bytes beyond the piece" (non-final piece).

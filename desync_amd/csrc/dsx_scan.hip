@@ -8,19 +8,24 @@
 // chain.
 //
 // MI355X mapping (DESIGN.md "Scan kernel"):
-//   * one workgroup = 8 waves, 1 per CU (160 KiB LDS), persistent over regions;
-//   * a wave owns a region of 64 lane segments of S bytes; lane l rolls the
-//     hash through its own segment, 48 bytes per round (one ring period);
-//   * HBM -> LDS with buffer_load_dwordx4 ... lds (LDS-DMA): each 1 KiB wave
-//     instruction fetches 21.3 lanes x 48 B, so every 128 B line is read once,
-//     4-deep ring per wave, no workgroup barrier in the loop;
+//   * one workgroup = 8 waves (2 per SIMD), 1 per CU (160 KiB LDS), persistent
+//     over regions; a wave owns a region of 64 lane segments of S bytes and
+//     lane l rolls the hash through its own segment;
+//   * HBM -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) in batches of 4
+//     rounds = 192 B per lane (12 KiB per wave): long per-lane runs keep DRAM
+//     and the texture path efficient (tools/ubench_staging.hip: 48 B rows
+//     4.0 TB/s, 192 B rows 6.3 TB/s); the batch is copied to registers at
+//     once so the next batch's DMA overlaps the hashing of this one;
 //   * the substitution table lives in LDS replicated over 32 lane slots
-//     (byte v, slot s at v*256 + s*8 = {T[v], rotl16(T[v])}) so the per-byte
-//     lookup is ONE v_perm_b32 (address = byte<<8 | slot) + ONE conflict-free
+//     (byte v, slot s at v*256 + s*8 = {T[v], rotl16(T[v])}) so each lookup is
+//     ONE v_perm_b32 (address = byte<<8 | slot) + ONE conflict-free
 //     ds_read_b64; the outgoing byte's rotated term comes from a 48-entry
-//     register ring (no second lookup);
-//   * the boundary test is a wave ballot per byte; rare hits leave the hot
-//     loop through one scalar branch per 16 bytes.
+//     register ring;
+//   * the boundary test is ONE cvt + ONE fma + ONE 24-bit mad + ONE compare
+//     (magic-number rounding, exact for 1024 < d < 2^22), a wave ballot per
+//     byte, and one scalar branch per 16 bytes for the rare hits;
+//   * at the end of a region the wave compacts its lanes' hits into one
+//     sorted per-region list for the stitch.
 #include <hip/hip_runtime.h>
 
 #include "../../include/dsx_buzhash_table.h"
@@ -31,11 +36,13 @@ namespace dsx {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+__constant__ uint32_t kT[256] = DSX_BUZHASH_TABLE_INIT;
+
 // One 1 KiB LDS-DMA wave instruction (buffer_load_dwordx4 ... lds): lane j's
-// 16 bytes from rsrc+voff land at LDS byte lds_addr + 16*j.  Written as inline
-// asm so that hipcc does not treat every later ds_read as aliasing a pending
-// DMA (it would emit s_waitcnt vmcnt(0) before each round and drain the
-// ring); completion is tracked by the explicit s_waitcnt vmcnt(N) in the loop.
+// 16 bytes from rsrc+voff land at LDS byte lds_addr + 16*j.  Inline asm so
+// hipcc does not treat later ds_reads as aliasing a pending DMA (it would
+// drain vmcnt(0) in front of unrelated LDS reads); completion is tracked by
+// the explicit s_waitcnt vmcnt(0) before a batch is read.
 __device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t lds_addr) {
   uint32_t keep;
   asm volatile(
@@ -49,12 +56,13 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t
       : "memory");
 }
 
-__constant__ uint32_t kT[256] = DSX_BUZHASH_TABLE_INIT;
-
-// h % d == d-1, evaluated on the GPU.
+// h % d == d-1 on the GPU.
 //   MODE 0: exactly Go's multiply-inverse form (chunker.go:265): v_mul_lo_u32.
-//   MODE 1: float-reciprocal quotient + exact 24-bit multiply check, valid for
-//           2048 < d < 2^24 (host chooses; see DESIGN.md "Boundary test").
+//   MODE 1: one fma lands h/d - (d-1)/d in [2^23, 2^24) where float spacing
+//           is 1, so the mantissa bits ARE round(q) (magic-number rounding);
+//           then the exact check h == q*d + d-1 with a 24-bit mad on those
+//           bits (the constant float offset is folded into tc.madc).
+//           Exact for 1024 < d < 2^22 (DESIGN.md "Boundary test").
 template <int MODE>
 __device__ __forceinline__ bool is_cand(uint32_t h, const TestConsts& tc) {
   if constexpr (MODE == 0) {
@@ -62,57 +70,129 @@ __device__ __forceinline__ bool is_cand(uint32_t h, const TestConsts& tc) {
     v = __builtin_amdgcn_alignbit(v, v, tc.rot);
     return v - tc.qbias <= tc.qmax;
   } else {
-    float f = __builtin_fmaf((float)h, tc.rcp, tc.c0);
-    uint32_t q = (uint32_t)f;
-    return __umul24(q, tc.d) + tc.dm1 == h;
+    const float f = __builtin_fmaf((float)h, tc.rcp, tc.c0);
+    const uint32_t bits = __builtin_bit_cast(uint32_t, f);
+    return __umul24(bits, tc.d) + tc.madc == h;
   }
 }
 
 // Process one 48-byte round of one lane.  `w` holds the round's bytes,
 // `ring[k]` the rotated table value of the byte 48 positions earlier.
-template <bool TEST, int MODE>
-__device__ __forceinline__ void round48(const uint32_t (&w)[12], uint32_t& h, uint32_t (&ring)[48],
+// The 48 bytes run as 6 subgroups of 8; the table lookups of subgroup j+1 are
+// issued before subgroup j is hashed (explicit software pipeline: the LDS
+// latency hides under the previous subgroup's hashing, and at most 16 LDS
+// reads are in flight, within the 4-bit lgkmcnt).
+// VARIANT (diagnostic ablations; results are wrong for VARIANT != 0):
+// 1 = no boundary test, 3 = staging only (no hashing).
+template <bool TEST, int MODE, int VARIANT>
+__device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t (&ring)[48],
                                         const uint8_t* __restrict__ tbl, uint32_t slot8,
                                         const TestConsts& tc, uint32_t lane, uint32_t obase,
                                         uint32_t seg_valid, uint32_t& cnt,
                                         uint16_t* __restrict__ myslots, uint32_t lane_slots) {
+  if constexpr (VARIANT == 3) {
 #pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    uint64_t m[16];
+    for (int k = 0; k < 12; ++k) h ^= w[k];
+    asm volatile("" ::"v"(h));
+    return;
+  }
+  constexpr int SUB = 8;
+  uint2 LA[SUB], LB[SUB];
+  auto issue = [&](int j, uint2 (&L)[SUB]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int k = g * 16 + i;
+    for (int i = 0; i < SUB; ++i) {
+      const int k = j * SUB + i;
       const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8);
       const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot8, sel);
-      const uint2 e = *reinterpret_cast<const uint2*>(tbl + addr);
-      h = __builtin_amdgcn_alignbit(h, h, 31) ^ e.x ^ ring[k];
-      ring[k] = e.y;
-      if constexpr (TEST) m[i] = __ballot(is_cand<MODE>(h, tc));
+      L[i] = *reinterpret_cast<const uint2*>(tbl + addr);
     }
-    if constexpr (TEST) {
-      uint64_t any = 0;
+  };
+  uint64_t m[16];
+  auto compute = [&](int j, uint2 (&L)[SUB]) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) any |= m[i];
-      if (__builtin_expect(any != 0, 0)) {
+    for (int i = 0; i < SUB; ++i) {
+      const int k = j * SUB + i;
+      // rotl1(h) ^ (T[in] ^ Trot[out]); the asm fence keeps the compiler from
+      // re-associating the second xor back onto the h chain
+      uint32_t x = L[i].x ^ ring[k];
+      asm("" : "+v"(x));
+      h = __builtin_amdgcn_alignbit(h, h, 31) ^ x;
+      ring[k] = L[i].y;
+      if constexpr (TEST && VARIANT == 0) m[k & 15] = __ballot(is_cand<MODE>(h, tc));
+    }
+    if constexpr (TEST && VARIANT != 0) {
+      asm volatile("" ::"v"(h));  // keep the ablated chain live (no DCE)
+    } else if constexpr (TEST) {
+      if ((j & 1) == 1) {  // rare-hit check once per 16 bytes
+        const int g = j >> 1;
+        uint64_t any = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if ((m[i] >> lane) & 1ull) {
-            const uint32_t o = obase + (uint32_t)(g * 16 + i) + 1u;  // offset in lane seg
-            if (o <= seg_valid) {
-              if (cnt < lane_slots) myslots[cnt] = (uint16_t)o;
-              ++cnt;
+        for (int i = 0; i < 16; ++i) any |= m[i];
+        if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            if ((m[i] >> lane) & 1ull) {
+              const uint32_t o = obase + (uint32_t)(g * 16 + i) + 1u;  // offset in lane seg
+              if (o <= seg_valid) {
+                if (cnt < lane_slots) myslots[cnt] = (uint16_t)o;
+                ++cnt;
+              }
             }
           }
         }
       }
     }
-  }
+  };
+  issue(0, LA);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(1, LB);
+  __builtin_amdgcn_sched_barrier(0);
+  compute(0, LA);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(2, LA);
+  __builtin_amdgcn_sched_barrier(0);
+  compute(1, LB);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(3, LB);
+  __builtin_amdgcn_sched_barrier(0);
+  compute(2, LA);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(4, LA);
+  __builtin_amdgcn_sched_barrier(0);
+  compute(3, LB);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(5, LB);
+  __builtin_amdgcn_sched_barrier(0);
+  compute(4, LA);
+  __builtin_amdgcn_sched_barrier(0);
+  compute(5, LB);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int MODE>
+// BR rounds per LDS-DMA batch (rows of BR*48 B per lane), NBUF LDS buffers per
+// wave: (4,1) = 192 B rows copied to registers at once; (2,2) = 96 B rows,
+// double-buffered in LDS.  Both use 96 KiB of staging.
+template <int MODE, int VARIANT, int BR, int NBUF>
 __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
+  constexpr int BB = BR * kRound;        // batch bytes per lane
+  constexpr int NC = BB / 16;            // 16 B chunks per lane row
+  constexpr int NI = kWave * BB / 1024;  // DMA wave instructions per batch
+  constexpr int STG = kWave * BB;        // staging bytes per buffer
+  static_assert(kTableBytes + kScanWaves * NBUF * STG <= kScanLds, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t lds[kScanLds];
 
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *a.overflow_next = 0u;  // parity buffer of the next piece (no reader now)
+    if (a.state_init) {     // first piece of a call: reset the chain state
+      uint64_t* st = (uint64_t*)a.state_init;
+      st[0] = a.init_carry;  // DevState.carry
+      st[1] = 0;             // total
+      st[2] = 0;             // piece_cuts
+      st[3] = 0;             // repaired
+      st[4] = 0;             // done, err
+      st[5] = 0;             // active, pad
+    }
+  }
   // ---- replicate {T, rotl16(T)} over 32 lane slots (64 KiB) ----
   for (int e = threadIdx.x; e < 256 * 32; e += kScanThreads) {
     const uint32_t v = kT[e >> 5];
@@ -126,20 +206,30 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t slot8 = (lane & 31u) * 8u;
-  uint8_t* stage = lds + kTableBytes + wave * (kNBuf * kStageBytes);
-  const uint32_t stage_lds = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(lds_void_t*)stage);
+  uint8_t* stage = lds + kTableBytes + wave * (NBUF * STG);
+  const uint32_t stage_lds =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)stage);
   const uint32_t S = a.lane_bytes;
-  const uint32_t R = a.rounds;
+  const uint32_t NB = a.batches;  // batches of BR rounds, warm-up round included
 
-  // DMA geometry: instruction i (0..2), lane j -> 16 B unit u = 64i + j of the
-  // 64 x 48 B round image: row u/3, chunk u%3.
-  uint32_t dma_row_off[3];
+  // DMA geometry: instruction i (0..NI-1), lane j -> 16 B unit u = 64i + j of
+  // the 64 x BB batch image: row u/NC, physical chunk u%NC.  Rows are stored
+  // rotated so that the ds_read_b128 row reads are bank-conflict free: chunk c
+  // of lane l lives at l*BB + ((c + rot(l)) % NC)*16 with rot(l) = (l>>2)%12
+  // for 12-chunk rows and (l>>4)%6 for 6-chunk rows (exhaustive search over
+  // the ds_read_b128 lane groups, DESIGN.md "Scan kernel").
+  auto rot_of = [](uint32_t l) -> uint32_t {
+    return NC == 12 ? (l >> 2) % 12u : (NC == 6 ? (l >> 4) % 6u : 0u);
+  };
+  uint32_t dma_off[NI];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const uint32_t u = (uint32_t)i * 64u + lane;
-    dma_row_off[i] = (u / 3u) * S + (u % 3u) * 16u;
+    const uint32_t row = u / (uint32_t)NC, phys = u % (uint32_t)NC;
+    const uint32_t c = (phys + (uint32_t)NC - rot_of(row)) % (uint32_t)NC;
+    dma_off[i] = row * S + c * 16u;
   }
+  const uint32_t rot = rot_of(lane);
 
   for (uint32_t region = blockIdx.x * kScanWaves + wave; region < a.nregions;
        region += gridDim.x * kScanWaves) {
@@ -150,7 +240,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     const uint32_t H = (rbase + a.halo >= (uint64_t)kRound) ? (uint32_t)kRound
                                                              : (uint32_t)(rbase + a.halo);
     const uint8_t* rptr = a.base + rbase - H;
-    uint64_t nrec64 = a.len - rbase + H;
+    const uint64_t nrec64 = a.len - rbase + H;
     const uint32_t nrec = nrec64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nrec64;
     const uint64_t rp = (uint64_t)(uintptr_t)rptr;
     u32x4 rsrc;
@@ -158,24 +248,21 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     rsrc.y = __builtin_amdgcn_readfirstlane((uint32_t)(rp >> 32) & 0xFFFFu);  // stride 0
     rsrc.z = __builtin_amdgcn_readfirstlane(nrec);
     rsrc.w = 0x00020000u;
-    // offset of round ri's chunk: row*S + chunk*16 + (ri+1)*48 + H - 48
-    const uint32_t hfix = H - (uint32_t)kRound;  // 0, or negative (wraps -> out of range)
-
-    auto issue = [&](int ri) {  // ri in [-1, R)
-      const uint32_t dst = stage_lds + ((uint32_t)(ri + 1) % kNBuf) * kStageBytes;
+    // batch b covers lane bytes [b*BB - 48, b*BB + BB - 48): buffer offset
+    // row*S + b*BB + chunk*16 + (H - 48) (negative wraps -> out of range -> 0)
+    const uint32_t hfix = H - (uint32_t)kRound;
+    auto issue = [&](uint32_t b) {
+      const uint32_t dst = stage_lds + (b % NBUF) * (uint32_t)STG;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        uint32_t vo = (ri < (int)R) ? dma_row_off[i] + (uint32_t)(ri + 1) * 48u + hfix
-                                    : 0xFFFFFFF0u;
+      for (int i = 0; i < NI; ++i) {
+        const uint32_t vo = (b < NB) ? dma_off[i] + b * (uint32_t)BB + hfix : 0xFFFFFFF0u;
         dma16(rsrc, vo, dst + (uint32_t)i * 1024u);
       }
     };
 
     // lane state
     const uint64_t lane_rel = rbase + (uint64_t)lane * S;  // piece-relative lane base
-    // valid offsets o (position = lane base + o) must stay inside the piece and
-    // beyond absolute position 48 (no full window before that).
-    uint32_t seg_valid = 0;
+    uint32_t seg_valid = 0;  // offsets o (p = lane base + o) must stay in the piece
     if (lane_rel < a.len) {
       const uint64_t rem = a.len - lane_rel;
       seg_valid = rem < S ? (uint32_t)rem : S;
@@ -183,64 +270,92 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     uint32_t cnt = 0;
     const uint64_t gl = (uint64_t)region * 64u + lane;
     uint16_t* myslots = a.lane_slot + gl * a.lane_slots;
-    const uint64_t lane_abs = a.piece_abs + lane_rel;
-    // p = lane_abs + o must be >= min_pos: windows before the chain origin are
-    // not real (virtual zero bytes at the blob/stream start)
-    const uint32_t o_min = lane_abs >= a.min_pos ? 0u : (uint32_t)(a.min_pos - lane_abs);
 
     uint32_t h = 0;
     uint32_t ring[48];
 #pragma unroll
     for (int k = 0; k < 48; ++k) ring[k] = 0;
 
-    issue(-1);
-    issue(0);
-    issue(1);
-    issue(2);
-    for (int ri = -1; ri < (int)R; ++ri) {
-      asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-      const uint8_t* src = stage + ((uint32_t)(ri + 1) % kNBuf) * kStageBytes + lane * 48u;
-      uint32_t w[12];
-      {
-        const uint4 q0 = *reinterpret_cast<const uint4*>(src);
-        const uint4 q1 = *reinterpret_cast<const uint4*>(src + 16);
-        const uint4 q2 = *reinterpret_cast<const uint4*>(src + 32);
-        w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w;
-        w[4] = q1.x; w[5] = q1.y; w[6] = q1.z; w[7] = q1.w;
-        w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+#pragma unroll
+    for (int q = 0; q < NBUF; ++q) issue((uint32_t)q);
+    for (uint32_t b = 0; b < NB; ++b) {
+      // batch b has landed once at most NBUF-1 younger batches are pending
+      if constexpr (NBUF == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (NBUF - 1)) : "memory");
+      }
+      const uint8_t* my_row = stage + (b % NBUF) * STG + lane * (uint32_t)BB;
+      uint32_t w[BR * 12];  // BR rounds x 12 dwords
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint32_t pc = (uint32_t)c + rot < (uint32_t)NC ? (uint32_t)c + rot
+                                                              : (uint32_t)c + rot - (uint32_t)NC;
+        const uint4 q = *reinterpret_cast<const uint4*>(my_row + pc * 16u);
+        w[4 * c] = q.x;
+        w[4 * c + 1] = q.y;
+        w[4 * c + 2] = q.z;
+        w[4 * c + 3] = q.w;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue(ri + 4);  // refill the buffer just read
-      if (ri < 0) {
-        round48<false, MODE>(w, h, ring, lds, slot8, a.tc, lane, 0u, 0u, cnt, myslots, 0u);
-      } else {
-        const uint32_t obase = (uint32_t)ri * 48u;
-        // positions <= 48 (absolute) are not real windows: clamp via seg_valid lower bound
-        round48<true, MODE>(w, h, ring, lds, slot8, a.tc, lane, obase, seg_valid, cnt, myslots,
-                           a.lane_slots);
+      issue(b + NBUF);  // refill the buffer just copied; lands during hashing
+#pragma unroll
+      for (int r = 0; r < BR; ++r) {
+        const int ri = (int)(b * BR) + r - 1;  // round index, -1 = warm-up
+        if (ri < 0) {
+          round48<false, MODE, VARIANT>(w + 12 * r, h, ring, lds, slot8, a.tc, lane, 0u, 0u, cnt,
+                                        myslots, 0u);
+        } else {
+          round48<true, MODE, VARIANT>(w + 12 * r, h, ring, lds, slot8, a.tc, lane,
+                                       (uint32_t)ri * 48u, seg_valid, cnt, myslots,
+                                       a.lane_slots);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (o_min > 0) {  // drop candidates before min_pos (chain origin only)
-      uint32_t keep = 0;
-      const uint32_t n = cnt < a.lane_slots ? cnt : a.lane_slots;
-      for (uint32_t i = 0; i < n; ++i) {
-        const uint16_t o = myslots[i];
-        if (o >= o_min) myslots[keep++] = o;
-      }
-      cnt = cnt - (n - keep);
+
+    // ---- region end: compact the lanes' hits into one sorted region list ----
+    // (slots were written by this lane in the rare path; candidates before
+    // min_pos -- windows reaching before the chain origin -- are dropped)
+    const uint64_t lane_abs = a.piece_abs + lane_rel;
+    const uint32_t o_min = lane_abs >= a.min_pos ? 0u : (uint32_t)(a.min_pos - lane_abs);
+    const uint32_t n = cnt < a.lane_slots ? cnt : a.lane_slots;
+    uint32_t keep = 0;
+    for (uint32_t i = 0; i < n; ++i) keep += myslots[i] >= o_min ? 1u : 0u;
+    uint32_t incl = keep;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += v;
     }
-    a.lane_cnt[gl] = cnt;
-    if (cnt > a.lane_slots) atomicAdd(a.overflow, 1u);
+    const uint32_t excl = incl - keep;
+    uint32_t exact = cnt - (n - keep);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) exact += __shfl_xor(exact, d, 64);
+    uint32_t* rl = a.region_list + (uint64_t)region * a.region_cap;
+    for (uint32_t i = 0, j = 0; i < n; ++i) {
+      const uint16_t o = myslots[i];
+      if (o >= o_min) {
+        if (excl + j < a.region_cap) rl[excl + j] = lane * S + o;
+        ++j;
+      }
+    }
+    const bool lane_ovf = __ballot(cnt > a.lane_slots) != 0;
+    if (lane == 0) {
+      a.region_cnt[region] = exact;
+      if (lane_ovf || exact > a.region_cap) atomicAdd(a.overflow, 1u);
+    }
   }
 }
 
-template __global__ void scan_kernel<0>(ScanArgs);
-template __global__ void scan_kernel<1>(ScanArgs);
+#define DSX_SCAN_INST(BR, NBUF)                                   \
+  template __global__ void scan_kernel<0, 0, BR, NBUF>(ScanArgs); \
+  template __global__ void scan_kernel<1, 0, BR, NBUF>(ScanArgs); \
+  template __global__ void scan_kernel<1, 1, BR, NBUF>(ScanArgs); \
+  template __global__ void scan_kernel<1, 3, BR, NBUF>(ScanArgs);
+DSX_SCAN_INST(4, 1)
+DSX_SCAN_INST(2, 2)
 
-}  // namespace dsx
-
-namespace dsx {
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1
 // (the plain form of chunker_test.go:190-213).  Diagnostic entry point.
 __global__ void boundary_selftest_kernel(TestConsts tc, int mode, uint64_t h0, uint64_t n,
@@ -255,4 +370,5 @@ __global__ void boundary_selftest_kernel(TestConsts tc, int mode, uint64_t h0, u
   }
   if (bad) atomicAdd(mismatches, bad);
 }
+
 }  // namespace dsx

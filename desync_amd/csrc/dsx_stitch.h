@@ -5,15 +5,16 @@
 
 namespace dsx {
 
-// Where a piece's candidates live: per-lane slot lists written by the scan.
-// Lane gl covers positions (P + gl*S, P + (gl+1)*S]; candidate = base + slot.
+// Where a piece's candidates live: sorted per-region lists written by the
+// scan.  Region r covers positions (P + r*RB, P + (r+1)*RB]; candidate =
+// P + r*RB + list entry.
 struct PieceCands {
   uint64_t P;             // absolute position of the piece's first byte
-  uint64_t nlanes;
-  uint32_t S;             // lane segment bytes
-  uint32_t lane_slots;    // slot capacity per lane (LS)
-  const uint32_t* lane_cnt;
-  const uint16_t* lane_slot;
+  uint64_t RB;            // region bytes (64 * lane segment)
+  uint32_t nregions;
+  uint32_t region_cap;
+  const uint32_t* region_cnt;
+  const uint32_t* region_list;
   const uint32_t* overflow;
 };
 
@@ -50,6 +51,13 @@ struct DevState {
   uint32_t active;      // current piece was processed (K3 ran its body)
   uint32_t pad;
 };
+
+// Published by the last kernel of a piece into pinned host memory.
+struct HostState {
+  uint64_t carry, total, repaired;
+  uint32_t done, err;
+  uint64_t seq;  // piece sequence number, for the host to check freshness
+};
 constexpr uint32_t kErrCapacity = 1u;  // output capacity exceeded
 constexpr uint32_t kErrDense = 2u;     // a lane overflowed its candidate slots
 
@@ -74,6 +82,8 @@ struct StitchArgs {
   uint64_t* out;     // contiguous cut list (device)
   uint64_t out_cap;
   DevState* state;
+  HostState* host_state;  // pinned, written by fixup_kernel (may be null)
+  uint64_t seq;
 };
 
 }  // namespace dsx

@@ -61,24 +61,28 @@ struct LdsSrc {
   }
 };
 
-// Candidates straight from the scan's per-lane slot lists (global memory);
-// used by the sequential repair only.
+// Candidates straight from the scan's per-region sorted lists (global
+// memory); used by the sequential repair only.
 struct GlobalSrc {
   const PieceCands* pc;
   __device__ uint64_t first_in(uint64_t a, uint64_t b) const {
-    // lane gl covers positions (P + gl*S, P + (gl+1)*S]
     if (b <= pc->P) return kNone;
-    const uint64_t lo_pos = a < pc->P ? pc->P : a;
-    uint64_t gl = (lo_pos - pc->P) / pc->S;
-    const uint64_t gl_end = (b - pc->P - 1) / pc->S;
-    for (; gl <= gl_end && gl < pc->nlanes; ++gl) {
-      const uint32_t cnt = pc->lane_cnt[gl];
-      const uint32_t n = cnt < pc->lane_slots ? cnt : pc->lane_slots;
-      const uint64_t base = pc->P + gl * (uint64_t)pc->S;
-      const uint16_t* sl = pc->lane_slot + gl * (uint64_t)pc->lane_slots;
-      for (uint32_t i = 0; i < n; ++i) {
-        const uint64_t p = base + sl[i];
-        if (p > a) return p <= b ? p : kNone;
+    const uint64_t pos = a < pc->P ? pc->P : a;
+    for (uint64_t r = (pos - pc->P) / pc->RB; r < pc->nregions; ++r) {
+      const uint64_t base = pc->P + r * pc->RB;  // region covers (base, base + RB]
+      if (base >= b) break;
+      const uint32_t cnt = pc->region_cnt[r];
+      const uint32_t n = cnt < pc->region_cap ? cnt : pc->region_cap;
+      const uint32_t* l = pc->region_list + r * (uint64_t)pc->region_cap;
+      const uint64_t ar = a > base ? a - base : 0;  // want entry > ar
+      uint32_t lo = 0, hi = n;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if ((uint64_t)l[m] <= ar) lo = m + 1; else hi = m;
+      }
+      if (lo < n) {
+        const uint64_t p = base + l[lo];
+        return p <= b ? p : kNone;
       }
     }
     return kNone;
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   __shared__ uint32_t s_total;
 
   const DevState* st = a.state;
-  if (st->done || *a.pc.overflow) return;  // finished, or scan slots overflowed
+  if (st->done || *a.pc.overflow) return;  // finished, or scan lists overflowed
   const uint64_t s0 = st->carry;
   const uint32_t kA = blockIdx.x * a.spg;
   if (kA >= a.nseg) return;
@@ -131,25 +135,20 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   const uint64_t hi = seg_end(a, kB);
   const PieceCands& pc = a.pc;
 
-  // ---- gather candidates in (lo, hi] into LDS, sorted (lane order) ----
-  uint64_t gl0 = lo <= pc.P ? 0 : (lo - pc.P) / pc.S;
-  uint64_t gl1 = hi <= pc.P ? 0 : (hi - pc.P - 1) / pc.S + 1;  // exclusive
-  if (gl1 > pc.nlanes) gl1 = pc.nlanes;
-  if (gl0 > gl1) gl0 = gl1;
-  const uint64_t nl = gl1 - gl0;
-  const uint64_t per = (nl + kWalkThreads - 1) / kWalkThreads;
-  const uint64_t my0 = gl0 + (uint64_t)threadIdx.x * per;
-  const uint64_t my1 = (my0 + per < gl1) ? my0 + per : gl1;
-  uint32_t mine = 0;
-  for (uint64_t g = my0; g < my1; ++g) {
-    const uint32_t c = pc.lane_cnt[g];
-    mine += c < pc.lane_slots ? c : pc.lane_slots;
+  // ---- gather candidates in (lo, hi] into LDS, sorted (region order) ----
+  const uint64_t r0 = lo <= pc.P ? 0 : (lo - pc.P) / pc.RB;
+  uint64_t r1 = hi <= pc.P ? 0 : (hi - pc.P - 1) / pc.RB + 1;  // exclusive
+  if (r1 > pc.nregions) r1 = pc.nregions;
+  const uint32_t nreg = r1 > r0 ? (uint32_t)(r1 - r0) : 0u;
+  bool dense = nreg > kWalkThreads;
+  if (!dense && threadIdx.x < nreg) {
+    const uint32_t c = pc.region_cnt[r0 + threadIdx.x];
+    s_part[threadIdx.x] = c < pc.region_cap ? c : pc.region_cap;
   }
-  s_part[threadIdx.x] = mine;
   __syncthreads();
-  if (threadIdx.x == 0) {  // tiny serial scan over 256 partials
+  if (threadIdx.x == 0) {  // tiny serial scan over the WG's regions
     uint32_t acc = 0;
-    for (int i = 0; i < kWalkThreads; ++i) {
+    for (uint32_t i = 0; i < nreg && i < kWalkThreads; ++i) {
       const uint32_t v = s_part[i];
       s_part[i] = acc;
       acc += v;
@@ -158,19 +157,18 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   }
   __syncthreads();
   const uint32_t total = s_total;
-  const bool dense = total > a.lds_cap;
-  if (!dense) {
+  dense = dense || total > a.lds_cap;
+  if (!dense && threadIdx.x < nreg) {
+    const uint64_t r = r0 + threadIdx.x;
+    const uint32_t c = pc.region_cnt[r];
+    const uint32_t n = c < pc.region_cap ? c : pc.region_cap;
+    const uint64_t base = pc.P + r * pc.RB;
+    const uint32_t* l = pc.region_list + r * (uint64_t)pc.region_cap;
     uint32_t o = s_part[threadIdx.x];
-    for (uint64_t g = my0; g < my1; ++g) {
-      const uint32_t c = pc.lane_cnt[g];
-      const uint32_t n = c < pc.lane_slots ? c : pc.lane_slots;
-      const uint64_t base = pc.P + g * (uint64_t)pc.S;
-      const uint16_t* sl = pc.lane_slot + g * (uint64_t)pc.lane_slots;
-      for (uint32_t i = 0; i < n; ++i) {
-        const uint64_t p = base + sl[i];
-        // keep the array sorted: below-range -> 0, above-range -> UINT32_MAX
-        cand[o++] = p <= lo ? 0u : (p > hi ? 0xFFFFFFFFu : (uint32_t)(p - lo));
-      }
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint64_t p = base + l[i];
+      // keep the array sorted: below-range -> 0, above-range -> UINT32_MAX
+      cand[o++] = p <= lo ? 0u : (p > hi ? 0xFFFFFFFFu : (uint32_t)(p - lo));
     }
   }
   __syncthreads();
@@ -240,6 +238,20 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
 // ---- K3: validity propagation, sequential repair, scan of counts ----------
 constexpr int kFixThreads = 1024;
 
+// Mirror the chain state into pinned host memory (the host reads it after the
+// stream synchronises, no D2H copy needed).
+__device__ void publish(const StitchArgs& a, const DevState* st) {
+  if (!a.host_state) return;
+  volatile HostState* h = a.host_state;
+  h->carry = st->carry;
+  h->total = st->total;
+  h->repaired = st->repaired;
+  h->done = st->done;
+  h->err = st->err;
+  h->seq = a.seq;
+  __threadfence_system();
+}
+
 __device__ uint32_t bsearch_u64(const uint64_t* v, uint32_t n, uint64_t x) {
   uint32_t l = 0, h = n;
   while (l < h) {
@@ -251,7 +263,7 @@ __device__ uint32_t bsearch_u64(const uint64_t* v, uint32_t n, uint64_t x) {
 
 __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
   __shared__ uint32_t s_flag_cnt;
-  __shared__ uint64_t s_part[kFixThreads];
+  __shared__ uint64_t s_part[kFixThreads / 64];
   __shared__ int s_last_seg;
   DevState* st = a.state;
   if (st->done || *a.pc.overflow) {
@@ -259,6 +271,7 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
       st->active = 0;
       st->piece_cuts = 0;
       if (*a.pc.overflow) st->err |= kErrDense;
+      publish(a, st);
     }
     return;
   }
@@ -347,7 +360,7 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
   }
   __syncthreads();
 
-  // (3) per-segment final counts -> exclusive scan -> output offsets
+  // (3) per-segment final counts -> exclusive block scan -> output offsets
   const uint32_t per = (T + kFixThreads - 1) / kFixThreads;
   const uint32_t k0 = threadIdx.x * per < T ? threadIdx.x * per : T;
   const uint32_t k1 = (k0 + per < T) ? k0 + per : T;
@@ -360,13 +373,21 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
     mine += c;
     if (c > 0) last_nonempty = (int)k;
   }
-  s_part[threadIdx.x] = mine;
   if (threadIdx.x == 0) s_last_seg = -1;
+  // wave-level inclusive scan, then a scan over the 16 wave totals
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t v = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  if (lane == 63) s_part[wv] = incl;
   __syncthreads();
   atomicMax(&s_last_seg, last_nonempty);
   if (threadIdx.x == 0) {
     uint64_t acc = 0;
-    for (int i = 0; i < kFixThreads; ++i) {
+    for (int i = 0; i < kFixThreads / 64; ++i) {
       const uint64_t v = s_part[i];
       s_part[i] = acc;
       acc += v;
@@ -374,7 +395,7 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
     st->piece_cuts = acc;
   }
   __syncthreads();
-  uint64_t off = st->total + s_part[threadIdx.x];
+  uint64_t off = st->total + s_part[wv] + (incl - mine);
   for (uint32_t k = k0; k < k1; ++k) {
     const SegInfo& si = a.seg_info[k];
     const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
@@ -397,6 +418,7 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
     if (tot > a.out_cap) st->err |= kErrCapacity;
     st->total = tot;
     st->active = 1;
+    publish(a, st);
   }
 }
 

@@ -1,0 +1,137 @@
+// ubench_staging.hip -- how fast can each lane stream its own contiguous
+// segment (the scan kernel's access pattern) into registers?  Standalone
+// microbenchmark (tools/, not part of libdsx).  Each kernel XORs the words it
+// receives so the loads stay live; prints GB/s per variant.
+//   hipcc --offload-arch=gfx950 -O3 tools/ubench_staging.hip -o /tmp/ubench
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <vector>
+
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(lds_addr), "s"(rsrc) : "memory");
+}
+
+// plain coalesced streaming read (HBM ceiling)
+__global__ void k_copy(const uint4* p, uint64_t n16, uint32_t* out) {
+  uint32_t acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4 v = p[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678) out[0] = acc;
+}
+
+// per-lane segments of S bytes, register loads, DEPTH rounds of 48 B in flight
+template <int DEPTH>
+__global__ __launch_bounds__(1024) void k_reg(const uint8_t* base, uint32_t S, uint32_t nregions, uint32_t* out) {
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t waves = blockDim.x >> 6;
+  uint32_t acc = 0;
+  const uint32_t R = S / 48;
+  for (uint32_t region = blockIdx.x * waves + wave; region < nregions; region += gridDim.x * waves) {
+    const u32x4* p = (const u32x4*)(base + ((uint64_t)region * 64 + lane) * S);
+    u32x4 buf[DEPTH][3];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) buf[d][c] = __builtin_nontemporal_load(p + d * 3 + c);
+    for (uint32_t r = 0; r < R; r += DEPTH) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          acc ^= buf[d][c].x ^ buf[d][c].y ^ buf[d][c].z ^ buf[d][c].w;
+          const uint32_t nr = r + d + DEPTH;
+          if (nr < R) buf[d][c] = __builtin_nontemporal_load(p + nr * 3 + c);
+        }
+      }
+    }
+  }
+  if (acc == 0x12345678) out[0] = acc;
+}
+
+// per-lane segments, LDS-DMA rows of ROWB bytes (multiple of 48), NB buffers
+template <int ROWB, int NB, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_dma(const uint8_t* base, uint32_t S, uint32_t nregions, uint64_t len, uint32_t* out) {
+  constexpr int BUF = 64 * ROWB;
+  constexpr int NI = BUF / 1024;  // DMA instructions per batch
+  __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * NB * BUF];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint8_t* stage = lds + wave * NB * BUF;
+  const uint32_t stage_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)stage);
+  uint32_t acc = 0;
+  const uint32_t B = S / ROWB;  // batches per lane segment
+  uint32_t roff[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const uint32_t u = i * 64 + lane;
+    roff[i] = (u / (ROWB / 16)) * S + (u % (ROWB / 16)) * 16;
+  }
+  for (uint32_t region = blockIdx.x * WAVES + wave; region < nregions; region += gridDim.x * WAVES) {
+    const uint64_t rp = (uint64_t)(uintptr_t)(base + (uint64_t)region * 64 * S);
+    u32x4 rs;
+    rs.x = __builtin_amdgcn_readfirstlane((uint32_t)rp);
+    rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(rp >> 32) & 0xFFFF);
+    rs.z = 64u * S;
+    rs.w = 0x00020000u;
+    auto issue = [&](uint32_t b) {
+      const uint32_t dst = stage_lds + (b % NB) * BUF;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) dma16(rs, b < B ? roff[i] + b * ROWB : 0xFFFFFFF0u, dst + i * 1024);
+    };
+    for (int b = 0; b < NB - 1; ++b) issue(b);
+    for (uint32_t b = 0; b < B; ++b) {
+      if constexpr (NB == 8) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI * 6) : "memory");
+      else if constexpr (NB == 4) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI * 2) : "memory");
+      else if constexpr (NB == 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint4* src = (const uint4*)(stage + (b % NB) * BUF + lane * ROWB);
+#pragma unroll
+      for (int c = 0; c < ROWB / 16; ++c) { uint4 v = src[c]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(b + NB - 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (acc == 0x12345678) out[0] = acc;
+}
+
+int main() {
+  const uint64_t len = 1ull << 30;
+  uint8_t* d; uint32_t* o;
+  CHK(hipMalloc(&d, len + 4096)); CHK(hipMalloc(&o, 64));
+  CHK(hipMemset(d, 7, len));
+  int ncu = 256;
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  auto timeit = [&](const char* name, auto launch) {
+    for (int i = 0; i < 3; ++i) launch();
+    hipEventRecord(e0);
+    const int it = 10;
+    for (int i = 0; i < it; ++i) launch();
+    hipEventRecord(e1); hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    printf("%-40s %8.3f ms  %7.0f GB/s  %s\n", name, ms / it, len / (ms / it * 1e-3) / 1e9, hipGetErrorString(hipGetLastError()));
+  };
+  timeit("coalesced copy-read", [&] { k_copy<<<ncu * 8, 256>>>((const uint4*)d, len / 16, o); });
+  const uint32_t S = 8208;
+  const uint32_t nreg = (uint32_t)((len + 64ull * S - 1) / (64ull * S)) - 1;  // keep in bounds
+  timeit("dma rows48 nb4 8w (current)", [&] { k_dma<48, 4, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("dma rows96 nb3 8w", [&] { k_dma<96, 3, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("dma rows96 nb2 8w", [&] { k_dma<96, 2, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("dma rows96 nb3 6w", [&] { k_dma<96, 3, 6><<<ncu, 384>>>(d, S, nreg, len, o); });
+  timeit("dma rows144 nb2 8w", [&] { k_dma<144, 2, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("dma rows144 nb2 6w", [&] { k_dma<144, 2, 6><<<ncu, 384>>>(d, S, nreg, len, o); });
+  timeit("dma rows144 nb3 4w", [&] { k_dma<144, 3, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  timeit("dma rows192 nb2 4w", [&] { k_dma<192, 2, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  timeit("dma rows240 nb2 4w", [&] { k_dma<240, 2, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  timeit("dma rows96 nb4 4w", [&] { k_dma<96, 4, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  timeit("dma rows48 nb4 4w", [&] { k_dma<48, 4, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  timeit("dma rows48 nb8 4w", [&] { k_dma<48, 8, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  return 0;
+}
