@@ -25,7 +25,7 @@
 #include "dsx_stitch.h"
 
 namespace dsx {
-template <int MODE, int VARIANT, int BR, int NBUF>
+template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB>
 __global__ void scan_kernel(ScanArgs a);
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
@@ -50,8 +50,7 @@ constexpr uint64_t kPieceMax = 8ull << 30;       // bytes per scan launch
 constexpr uint64_t kHostChunk = 256ull << 20;    // host-resident pipeline chunk
 constexpr uint64_t kStreamBatch = 16ull << 20;   // streaming: bytes per device batch
 constexpr uint32_t kWalkLdsCap = 12288;          // candidates per walk workgroup
-constexpr uint32_t kDenseS = 48 * 11;            // dense path lane bytes (= slot cap), BR=4
-constexpr uint32_t kDenseS2 = 48 * 9;            // dense path lane bytes, BR=2
+constexpr uint32_t kDenseS = 48 * 9;             // dense path lane bytes (= slot cap)
 constexpr uint64_t kDensePiece = 32ull << 20;    // dense path piece size
 
 template <class T>
@@ -88,10 +87,11 @@ struct dsx_ctx {
   int force_mode = -1;  // DSX_TEST_MODE env override
   int variant = 0;      // DSX_SCAN_VARIANT: diagnostic scan ablations (wrong results)
   uint32_t lane_bytes_override = 0;  // DSX_LANE_BYTES (tuning; multiple of 48)
-  int batch_rounds = 4;               // DSX_BATCH_ROUNDS: scan staging (4x1 or 2x2)
+  int regions_per_slot = 4;           // DSX_REGIONS_PER_SLOT: scan work units per wave slot
+  int scan_cfg = 0;                   // DSX_SCAN_CFG: 0 = 8 waves x 2 LDS buffers, 1 = 12 x 1, 2 = 16 x 1
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
-  DevBuf<uint16_t> lane_slot;
+  DevBuf<uint32_t> lane_slot;
   DevBuf<SegInfo> seg_info;
   DevBuf<uint64_t> stage, rep, out_off, out;
   DevBuf<DevState> state;
@@ -271,7 +271,8 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   c->ncu = prop.multiProcessorCount;
   if (const char* m = getenv("DSX_TEST_MODE")) c->force_mode = atoi(m);
   if (const char* v = getenv("DSX_SCAN_VARIANT")) c->variant = atoi(v);
-  if (const char* v = getenv("DSX_BATCH_ROUNDS")) c->batch_rounds = atoi(v) == 2 ? 2 : 4;
+  if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
+  if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(2, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
     const long lb = atol(v);
     if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
@@ -288,8 +289,8 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
   memset(c->h_state, 0, sizeof(HostState));
   CREATE_STEP(c->state.ensure(1));
-  CREATE_STEP(c->overflow.ensure(2));
-  CREATE_STEP(hipMemset(c->overflow.p, 0, 2 * sizeof(uint32_t)));
+  CREATE_STEP(c->overflow.ensure(4));  // [0..1] overflow, [2..3] scan work queue (parity)
+  CREATE_STEP(hipMemset(c->overflow.p, 0, 4 * sizeof(uint32_t)));
   CREATE_STEP(hipMemset(c->state.p, 0, sizeof(DevState)));
 #undef CREATE_STEP
   *out = c;
@@ -373,16 +374,24 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   // ---- scan geometry: balance regions over the persistent grid ----
   // lane segment S = 48*(4k-1): the warm-up round plus S/48 rounds fill k
   // whole 4-round DMA batches
-  const uint64_t slots_total = (uint64_t)c->ncu * kScanWaves;  // wave slots
+  // scan configs: {waves per workgroup, rounds per DMA batch}
+  static const int kCfgWaves[3] = {8, 12, 16};
+  static const int kCfgBR[3] = {2, 1, 1};
+  const int W = kCfgWaves[c->scan_cfg];
+  const int cfgBR = kCfgBR[c->scan_cfg];
+  const uint64_t slots_total = (uint64_t)c->ncu * W;  // wave slots
   uint32_t S, LS;
   if (cc.dense) {
-    S = c->batch_rounds == 4 ? kDenseS : kDenseS2;
+    S = kDenseS;
     LS = S;
   } else {
-    const uint64_t per_lane = (len + slots_total * 64 - 1) / (slots_total * 64);
-    const uint64_t rounds_needed = (per_lane + kMaxLaneBytes - 1) / kMaxLaneBytes;  // waves/slot
-    uint64_t s = (len + rounds_needed * slots_total * 64 - 1) / (rounds_needed * slots_total * 64);
-    const uint64_t BR = (uint64_t)c->batch_rounds;
+    // about regions_per_slot regions per wave slot (dynamic queue balances
+    // them), more if a lane segment would exceed kMaxLaneBytes
+    const uint64_t lanes_min = slots_total * 64 * (uint64_t)c->regions_per_slot;
+    const uint64_t per_lane = (len + lanes_min - 1) / lanes_min;
+    const uint64_t rounds_needed = (per_lane + kMaxLaneBytes - 1) / kMaxLaneBytes;
+    uint64_t s = (len + rounds_needed * lanes_min - 1) / (rounds_needed * lanes_min);
+    const uint64_t BR = (uint64_t)cfgBR;
     uint64_t kb = (s / kRound + 1 + BR - 1) / BR;  // batches
     if (kb < 4) kb = 4;
     while (kRound * (BR * kb - 1) > kMaxLaneBytes) --kb;
@@ -392,7 +401,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     S = (uint32_t)s;
     LS = kLaneSlots;
   }
-  const uint32_t batches = (S / kRound + 1) / (uint32_t)c->batch_rounds;
+  const uint32_t batches = (S / kRound + 1) / (uint32_t)cfgBR;
   const uint64_t region_bytes = 64ull * S;
   const uint64_t nregions = len == 0 ? 0 : (len + region_bytes - 1) / region_bytes;
   const uint64_t nlanes = nregions * 64;
@@ -426,6 +435,8 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   sa.region_list = c->region_list.p;
   sa.overflow = c->overflow.p + (seq & 1);
   sa.overflow_next = c->overflow.p + ((seq + 1) & 1);
+  sa.queue = c->overflow.p + 2 + (seq & 1);
+  sa.queue_next = c->overflow.p + 2 + ((seq + 1) & 1);
   sa.state_init = c->init_pending ? (void*)c->state.p : nullptr;
   sa.init_carry = c->init_carry;
   c->init_pending = false;
@@ -437,25 +448,29 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   }
   HIPCHK(c, hipEventRecord(c->pev[3 * pi], c->stream));
   {
-    const uint64_t need_wg = std::max<uint64_t>(1, (nregions + kScanWaves - 1) / kScanWaves);
+    const uint64_t need_wg = std::max<uint64_t>(1, (nregions + W - 1) / W);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)c->ncu);
-    const dim3 g(grid), b(kScanThreads);
+    const dim3 g(grid), b(W * kWave);
     const int mode = pick_mode(c, p->discriminator);
-#define DSX_LAUNCH(BR, NB)                                                              \
-  do {                                                                                  \
-    if (c->variant == 1)                                                                \
-      hipLaunchKernelGGL((scan_kernel<1, 1, BR, NB>), g, b, 0, c->stream, sa);          \
-    else if (c->variant == 3)                                                           \
-      hipLaunchKernelGGL((scan_kernel<1, 3, BR, NB>), g, b, 0, c->stream, sa);          \
-    else if (mode == 1)                                                                 \
-      hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB>), g, b, 0, c->stream, sa);          \
-    else                                                                                \
-      hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB>), g, b, 0, c->stream, sa);          \
+#define DSX_LAUNCH(BR, NB, WV, SUB)                                                    \
+  do {                                                                                 \
+    if (c->variant == 1)                                                               \
+      hipLaunchKernelGGL((scan_kernel<1, 1, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+    else if (c->variant == 3)                                                          \
+      hipLaunchKernelGGL((scan_kernel<1, 3, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+    else if (c->variant == 4)                                                          \
+      hipLaunchKernelGGL((scan_kernel<1, 4, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+    else if (mode == 1)                                                                \
+      hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+    else                                                                               \
+      hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
   } while (0)
-    if (c->batch_rounds == 4)
-      DSX_LAUNCH(4, 1);
+    if (W == 8)
+      DSX_LAUNCH(2, 2, 8, 8);
+    else if (W == 12)
+      DSX_LAUNCH(1, 2, 12, 4);
     else
-      DSX_LAUNCH(2, 2);
+      DSX_LAUNCH(1, 2, 16, 4);
 #undef DSX_LAUNCH
     HIPCHK(c, hipGetLastError());
   }
@@ -1049,7 +1064,7 @@ extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
       if (rc) return rc;
       HIPCHK(c, hipStreamSynchronize(c->stream));
       // read back the region lists of the dense-path scan of the window
-      const uint64_t RB = 64ull * (c->batch_rounds == 4 ? kDenseS : kDenseS2);
+      const uint64_t RB = 64ull * kDenseS;
       const uint64_t nr = (wlen + RB - 1) / RB;
       const uint64_t cap = RB;  // dense path: region_cap == region bytes
       std::vector<uint32_t> cnt(nr);

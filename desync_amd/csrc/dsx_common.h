@@ -15,18 +15,15 @@ namespace dsx {
 
 constexpr int kWave = 64;
 // ---- scan kernel geometry (see DESIGN.md "Scan kernel") --------------------
-constexpr int kScanWaves = 8;                 // waves per workgroup (2 per SIMD)
-constexpr int kScanThreads = kScanWaves * kWave;
 constexpr int kRound = 48;                    // bytes per lane per round == window
-constexpr int kStageBytesPerWave = 12288;     // LDS-DMA staging per wave (BR*NBUF*48*64)
 constexpr int kTableBytes = 256 * 256;        // 256 byte values x 32 lane slots x {T,Trot}
-constexpr int kScanLds = kTableBytes + kScanWaves * kStageBytesPerWave;  // 163840
+constexpr int kScanLds = 163840;              // LDS per CU: table + per-wave staging
 constexpr int kLaneSlots = 32;                // candidate slots per lane segment
-// lane segment = 48*(BR*k-1) bytes (warm-up round + segment = whole batches);
+// lane segment = 48*(BR*k-1) bytes, BR = rounds per DMA batch (warm-up round +
+// segment = whole batches);
 // offsets stay in u16
-constexpr uint32_t kMaxLaneBytes = 48u * (4u * 341u - 1u);  // 65424
+constexpr uint32_t kMaxLaneBytes = 48u * (2u * 682u - 1u);  // 65424
 
-static_assert(kScanLds <= 163840, "scan LDS budget exceeds 160 KiB");
 
 // Division-free boundary test constants (host-computed, chunker.go:147-170).
 struct TestConsts {
@@ -55,11 +52,13 @@ struct ScanArgs {
   uint64_t min_pos;      // candidates at absolute p < min_pos are dropped (origin + 49)
   uint32_t lane_slots;   // slot capacity per lane (kLaneSlots, or S on the dense path)
   uint32_t pad2;
-  uint16_t* lane_slot;   // scratch [nregions*64*lane_slots]: per-lane hits (rare writes)
+  uint32_t* lane_slot;   // scratch [nregions*64*lane_slots]: per-lane hit entries (rare writes)
   uint32_t* region_cnt;  // [nregions] candidates per region (exact)
   uint32_t* region_list; // [nregions*region_cap] sorted offsets in (0, 64*S] from region base
   uint32_t* overflow;    // regions whose lanes or list overflowed (-> dense path)
   uint32_t* overflow_next;  // the next piece's counter: zeroed here (parity buffers)
+  uint32_t* queue;       // region work queue (regions beyond the first wave slot pass)
+  uint32_t* queue_next;  // the next piece's queue counter: zeroed here
   void* state_init;      // if non-null: DevState to initialise (first piece of a call)
   uint64_t init_carry;
 };

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/dsx_buzhash_table.h"
+#include <type_traits>
 #include "dsx_common.h"
 
 namespace dsx {
@@ -78,111 +79,111 @@ __device__ __forceinline__ bool is_cand(uint32_t h, const TestConsts& tc) {
 
 // Process one 48-byte round of one lane.  `w` holds the round's bytes,
 // `ring[k]` the rotated table value of the byte 48 positions earlier.
-// The 48 bytes run as 6 subgroups of 8; the table lookups of subgroup j+1 are
+// The 48 bytes run as 48/SUB subgroups; the table lookups of subgroup j+1 are
 // issued before subgroup j is hashed (explicit software pipeline: the LDS
-// latency hides under the previous subgroup's hashing, and at most 16 LDS
+// latency hides under the previous subgroup's hashing; at most 2*SUB LDS
 // reads are in flight, within the 4-bit lgkmcnt).
 // VARIANT (diagnostic ablations; results are wrong for VARIANT != 0):
-// 1 = no boundary test, 3 = staging only (no hashing).
-template <bool TEST, int MODE, int VARIANT>
+// 1 = no boundary test, 3 = staging only (no hashing), 4 = no staging (the
+// kernel hashes whatever the LDS holds: compute ceiling).
+template <int SUB>
+__device__ __forceinline__ void lookups_landed(uint64_t (&L)[SUB]) {
+  // the empty asm consumes all lookups of a subgroup, so the compiler emits a
+  // single s_waitcnt in front of it instead of one per use
+  if constexpr (SUB == 8) {
+    asm volatile("" : "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]), "+v"(L[4]), "+v"(L[5]),
+                 "+v"(L[6]), "+v"(L[7]));
+  } else {
+    static_assert(SUB == 4, "SUB is 4 or 8");
+    asm volatile("" : "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]));
+  }
+}
+
+template <bool TEST, int MODE, int VARIANT, int SUB>
 __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t (&ring)[48],
                                         const uint8_t* __restrict__ tbl, uint32_t slot8,
                                         const TestConsts& tc, uint32_t lane, uint32_t obase,
-                                        uint32_t seg_valid, uint32_t& cnt,
-                                        uint16_t* __restrict__ myslots, uint32_t lane_slots) {
+                                        uint32_t& cnt, uint32_t* __restrict__ myslots,
+                                        uint32_t lane_slots) {
   if constexpr (VARIANT == 3) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) h ^= w[k];
     asm volatile("" ::"v"(h));
     return;
   }
-  constexpr int SUB = 8;
-  uint2 LA[SUB], LB[SUB];
-  auto issue = [&](int j, uint2 (&L)[SUB]) {
+  constexpr int NSG = kRound / SUB;
+  uint64_t L[2][SUB];  // {T[in], rotl16(T[in])} lookups, double-buffered
+  auto issue = [&](int j) {
 #pragma unroll
     for (int i = 0; i < SUB; ++i) {
       const int k = j * SUB + i;
       const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8);
       const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot8, sel);
-      L[i] = *reinterpret_cast<const uint2*>(tbl + addr);
+      L[j & 1][i] = *reinterpret_cast<const uint64_t*>(tbl + addr);
     }
   };
-  uint64_t m[16];
-  auto compute = [&](int j, uint2 (&L)[SUB]) {
+  auto compute = [&](int j) {
+    lookups_landed<SUB>(L[j & 1]);
+    uint64_t m[SUB];
 #pragma unroll
     for (int i = 0; i < SUB; ++i) {
       const int k = j * SUB + i;
       // rotl1(h) ^ (T[in] ^ Trot[out]); the asm fence keeps the compiler from
       // re-associating the second xor back onto the h chain
-      uint32_t x = L[i].x ^ ring[k];
+      uint32_t x = (uint32_t)L[j & 1][i] ^ ring[k];
       asm("" : "+v"(x));
       h = __builtin_amdgcn_alignbit(h, h, 31) ^ x;
-      ring[k] = L[i].y;
-      if constexpr (TEST && VARIANT == 0) m[k & 15] = __ballot(is_cand<MODE>(h, tc));
+      ring[k] = (uint32_t)(L[j & 1][i] >> 32);
+      if constexpr (TEST && (VARIANT == 0 || VARIANT == 4)) m[i] = __ballot(is_cand<MODE>(h, tc));
     }
-    if constexpr (TEST && VARIANT != 0) {
+    if constexpr (TEST && VARIANT != 0 && VARIANT != 4) {
       asm volatile("" ::"v"(h));  // keep the ablated chain live (no DCE)
     } else if constexpr (TEST) {
-      if ((j & 1) == 1) {  // rare-hit check once per 16 bytes
-        const int g = j >> 1;
-        uint64_t any = 0;
+      // rare path, once per subgroup: a lane with hits appends one entry
+      // {hit bits << 16 | offset of the subgroup} (region end expands them)
+      uint64_t any = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) any |= m[i];
-        if (__builtin_expect(any != 0, 0)) {
+      for (int i = 0; i < SUB; ++i) any |= m[i];
+      if (__builtin_expect(any != 0, 0)) {
+        uint32_t bits = 0;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            if ((m[i] >> lane) & 1ull) {
-              const uint32_t o = obase + (uint32_t)(g * 16 + i) + 1u;  // offset in lane seg
-              if (o <= seg_valid) {
-                if (cnt < lane_slots) myslots[cnt] = (uint16_t)o;
-                ++cnt;
-              }
-            }
-          }
+        for (int i = 0; i < SUB; ++i) bits |= (uint32_t)((m[i] >> lane) & 1ull) << i;
+        if (bits) {
+          if (cnt < lane_slots) myslots[cnt] = (bits << 16) | (obase + (uint32_t)(j * SUB));
+          ++cnt;
         }
       }
     }
   };
-  issue(0, LA);
+  issue(0);
   __builtin_amdgcn_sched_barrier(0);
-  issue(1, LB);
-  __builtin_amdgcn_sched_barrier(0);
-  compute(0, LA);
-  __builtin_amdgcn_sched_barrier(0);
-  issue(2, LA);
-  __builtin_amdgcn_sched_barrier(0);
-  compute(1, LB);
-  __builtin_amdgcn_sched_barrier(0);
-  issue(3, LB);
-  __builtin_amdgcn_sched_barrier(0);
-  compute(2, LA);
-  __builtin_amdgcn_sched_barrier(0);
-  issue(4, LA);
-  __builtin_amdgcn_sched_barrier(0);
-  compute(3, LB);
-  __builtin_amdgcn_sched_barrier(0);
-  issue(5, LB);
-  __builtin_amdgcn_sched_barrier(0);
-  compute(4, LA);
-  __builtin_amdgcn_sched_barrier(0);
-  compute(5, LB);
-  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < NSG; ++j) {
+    if (j + 1 < NSG) issue(j + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(j);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 // BR rounds per LDS-DMA batch (rows of BR*48 B per lane), NBUF LDS buffers per
-// wave: (4,1) = 192 B rows copied to registers at once; (2,2) = 96 B rows,
-// double-buffered in LDS.  Both use 96 KiB of staging.
-template <int MODE, int VARIANT, int BR, int NBUF>
-__global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
+// wave, W waves per workgroup (one workgroup per CU: the 64 KiB table is
+// per workgroup).  With NBUF == 1 the row is copied to registers before the
+// refill is issued, so LDS + registers still double-buffer.
+template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB>
+__global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   constexpr int BB = BR * kRound;        // batch bytes per lane
   constexpr int NC = BB / 16;            // 16 B chunks per lane row
   constexpr int NI = kWave * BB / 1024;  // DMA wave instructions per batch
   constexpr int STG = kWave * BB;        // staging bytes per buffer
-  static_assert(kTableBytes + kScanWaves * NBUF * STG <= kScanLds, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kScanLds];
+  constexpr int LDSB = kTableBytes + W * NBUF * STG;
+  constexpr int NT = W * kWave;
+  static_assert(LDSB <= kScanLds, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
 
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *a.overflow_next = 0u;  // parity buffer of the next piece (no reader now)
+    *a.overflow_next = 0u;  // parity buffers of the next piece (no reader now)
+    *a.queue_next = 0u;
     if (a.state_init) {     // first piece of a call: reset the chain state
       uint64_t* st = (uint64_t*)a.state_init;
       st[0] = a.init_carry;  // DevState.carry
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     }
   }
   // ---- replicate {T, rotl16(T)} over 32 lane slots (64 KiB) ----
-  for (int e = threadIdx.x; e < 256 * 32; e += kScanThreads) {
+  for (int e = threadIdx.x; e < 256 * 32; e += NT) {
     const uint32_t v = kT[e >> 5];
     uint2 t;
     t.x = v;
@@ -230,9 +231,20 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     dma_off[i] = row * S + c * 16u;
   }
   const uint32_t rot = rot_of(lane);
+  // test constants: c0 and madc live in VGPRs for the whole kernel (each VALU
+  // instruction reads at most one SGPR; otherwise the compiler re-moves them
+  // into VGPRs before every use)
+  TestConsts tcv = a.tc;
+  asm volatile("" : "+v"(tcv.c0));
+  asm volatile("" : "+v"(tcv.madc));
 
-  for (uint32_t region = blockIdx.x * kScanWaves + wave; region < a.nregions;
-       region += gridDim.x * kScanWaves) {
+  // regions: the first one per wave statically, then from a work queue (the
+  // two waves sharing a SIMD progress at different rates: VALU arbitration
+  // favours the older one, so static equal shares leave a one-wave tail)
+  uint32_t region = blockIdx.x * W + wave;
+  while (region < a.nregions) {
+    uint32_t next_ticket = 0;
+    if (lane == 0) next_ticket = atomicAdd(a.queue, 1u);  // lands while this region runs
     const uint64_t rbase = (uint64_t)region * 64u * S;  // piece-relative
     // readable bytes before the region (fewer than 48 only at the chain origin,
     // where the missing window bytes are virtual zeros: those loads fall out of
@@ -252,6 +264,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     // row*S + b*BB + chunk*16 + (H - 48) (negative wraps -> out of range -> 0)
     const uint32_t hfix = H - (uint32_t)kRound;
     auto issue = [&](uint32_t b) {
+      if constexpr (VARIANT == 4) return;  // ablation: hash stale LDS, no HBM traffic
       const uint32_t dst = stage_lds + (b % NBUF) * (uint32_t)STG;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -269,7 +282,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     }
     uint32_t cnt = 0;
     const uint64_t gl = (uint64_t)region * 64u + lane;
-    uint16_t* myslots = a.lane_slot + gl * a.lane_slots;
+    uint32_t* myslots = a.lane_slot + gl * a.lane_slots;
 
     uint32_t h = 0;
     uint32_t ring[48];
@@ -278,7 +291,10 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
 
 #pragma unroll
     for (int q = 0; q < NBUF; ++q) issue((uint32_t)q);
-    for (uint32_t b = 0; b < NB; ++b) {
+    // one batch; the warm-up round (window fill, no test) is peeled into the
+    // first batch so the steady-state loop has no branch around the rounds
+    // (a branch lets the compiler hoist all of a round's table addresses)
+    auto batch = [&](uint32_t b, auto first) {
       // batch b has landed once at most NBUF-1 younger batches are pending
       if constexpr (NBUF == 1) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -301,17 +317,17 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
       issue(b + NBUF);  // refill the buffer just copied; lands during hashing
 #pragma unroll
       for (int r = 0; r < BR; ++r) {
-        const int ri = (int)(b * BR) + r - 1;  // round index, -1 = warm-up
-        if (ri < 0) {
-          round48<false, MODE, VARIANT>(w + 12 * r, h, ring, lds, slot8, a.tc, lane, 0u, 0u, cnt,
-                                        myslots, 0u);
+        if (decltype(first)::value && r == 0) {
+          round48<false, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane, 0u, cnt, myslots, 0u);
         } else {
-          round48<true, MODE, VARIANT>(w + 12 * r, h, ring, lds, slot8, a.tc, lane,
-                                       (uint32_t)ri * 48u, seg_valid, cnt, myslots,
-                                       a.lane_slots);
+          const uint32_t ri = b * (uint32_t)BR + (uint32_t)r - 1u;  // round index
+          round48<true, MODE, VARIANT, SUB>(w + 12 * r, h, ring, lds, slot8, tcv, lane, ri * 48u, cnt,
+                                       myslots, a.lane_slots);
         }
       }
-    }
+    };
+    batch(0u, std::true_type{});
+    for (uint32_t b = 1; b < NB; ++b) batch(b, std::false_type{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // ---- region end: compact the lanes' hits into one sorted region list ----
@@ -320,8 +336,18 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
     const uint64_t lane_abs = a.piece_abs + lane_rel;
     const uint32_t o_min = lane_abs >= a.min_pos ? 0u : (uint32_t)(a.min_pos - lane_abs);
     const uint32_t n = cnt < a.lane_slots ? cnt : a.lane_slots;
+    auto for_each_hit = [&](auto&& f) {
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t e = myslots[i];
+        const uint32_t base = e & 0xFFFFu;
+        for (uint32_t bits = e >> 16; bits; bits &= bits - 1u) {
+          const uint32_t o = base + (uint32_t)__builtin_ctz(bits) + 1u;  // offset in lane seg
+          if (o >= o_min && o <= seg_valid) f(o);
+        }
+      }
+    };
     uint32_t keep = 0;
-    for (uint32_t i = 0; i < n; ++i) keep += myslots[i] >= o_min ? 1u : 0u;
+    for_each_hit([&](uint32_t) { ++keep; });
     uint32_t incl = keep;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -329,32 +355,33 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(ScanArgs a) {
       if (lane >= (uint32_t)d) incl += v;
     }
     const uint32_t excl = incl - keep;
-    uint32_t exact = cnt - (n - keep);
+    uint32_t exact = keep;  // (a lane overflow below sends the piece to the dense path)
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) exact += __shfl_xor(exact, d, 64);
     uint32_t* rl = a.region_list + (uint64_t)region * a.region_cap;
-    for (uint32_t i = 0, j = 0; i < n; ++i) {
-      const uint16_t o = myslots[i];
-      if (o >= o_min) {
-        if (excl + j < a.region_cap) rl[excl + j] = lane * S + o;
-        ++j;
-      }
-    }
+    uint32_t j = 0;
+    for_each_hit([&](uint32_t o) {
+      if (excl + j < a.region_cap) rl[excl + j] = lane * S + o;
+      ++j;
+    });
     const bool lane_ovf = __ballot(cnt > a.lane_slots) != 0;
     if (lane == 0) {
       a.region_cnt[region] = exact;
       if (lane_ovf || exact > a.region_cap) atomicAdd(a.overflow, 1u);
     }
+    region = gridDim.x * W + __builtin_amdgcn_readfirstlane(next_ticket);
   }
 }
 
-#define DSX_SCAN_INST(BR, NBUF)                                   \
-  template __global__ void scan_kernel<0, 0, BR, NBUF>(ScanArgs); \
-  template __global__ void scan_kernel<1, 0, BR, NBUF>(ScanArgs); \
-  template __global__ void scan_kernel<1, 1, BR, NBUF>(ScanArgs); \
-  template __global__ void scan_kernel<1, 3, BR, NBUF>(ScanArgs);
-DSX_SCAN_INST(4, 1)
-DSX_SCAN_INST(2, 2)
+#define DSX_SCAN_INST(BR, NBUF, W, SUB)                                   \
+  template __global__ void scan_kernel<0, 0, BR, NBUF, W, SUB>(ScanArgs); \
+  template __global__ void scan_kernel<1, 0, BR, NBUF, W, SUB>(ScanArgs); \
+  template __global__ void scan_kernel<1, 1, BR, NBUF, W, SUB>(ScanArgs); \
+  template __global__ void scan_kernel<1, 3, BR, NBUF, W, SUB>(ScanArgs); \
+  template __global__ void scan_kernel<1, 4, BR, NBUF, W, SUB>(ScanArgs);
+DSX_SCAN_INST(2, 2, 8, 8)
+DSX_SCAN_INST(1, 2, 12, 4)
+DSX_SCAN_INST(1, 2, 16, 4)
 
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1
 // (the plain form of chunker_test.go:190-213).  Diagnostic entry point.
