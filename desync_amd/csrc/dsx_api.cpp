@@ -235,12 +235,25 @@ static TestConsts make_tc(const dsx_params_t* p) {
   tc.c0 = 12582911.0f;
   tc.madc = p->discriminator - 1u - (p->discriminator << 22);
   tc.pad = 0;
+  // MODE 2 prefilter: with d = 2^k * dodd, h + 1 = d*m (1 <= m <= 2^32/d)
+  // gives t = (h+1)*inv - 1 = 2^k*m - 1 < 2^k*floor(2^32/d) = vmax (exact
+  // for odd d; for even d the rare path re-checks h % d == d-1)
+  const uint32_t k = (uint32_t)p->rot;
+  tc.tadd = p->inverse_odd - 1u;
+  tc.vmax = (uint32_t)(((1ull << 32) / p->discriminator) << k);
+  tc.dodd = p->discriminator >> k;
+  tc.pad2 = 0;
   return tc;
 }
 
-// float magic-number test is exact for 1024 < d < 2^22 (DESIGN.md "Boundary test")
+// MODE 2 (multiply-inverse prefilter, DESIGN.md "Boundary test") for every d
+// that is not a power of two; MODE 1 (float, exact for 1024 < d < 2^22) or
+// MODE 0 (Go's form) otherwise
 static int pick_mode(const dsx_ctx* c, uint32_t d) {
-  if (c->force_mode == 0 || c->force_mode == 1) return c->force_mode;
+  if (c->force_mode >= 0 && c->force_mode <= 2) {
+    if (c->force_mode != 2 || (d & (d - 1u)) != 0) return c->force_mode;
+  }
+  if ((d & (d - 1u)) != 0) return 2;
   return (d > 1024u && d < (1u << 22)) ? 1 : 0;
 }
 
@@ -455,11 +468,13 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
 #define DSX_LAUNCH(BR, NB, WV, SUB)                                                    \
   do {                                                                                 \
     if (c->variant == 1)                                                               \
-      hipLaunchKernelGGL((scan_kernel<1, 1, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+      hipLaunchKernelGGL((scan_kernel<2, 1, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
     else if (c->variant == 3)                                                          \
-      hipLaunchKernelGGL((scan_kernel<1, 3, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+      hipLaunchKernelGGL((scan_kernel<2, 3, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
     else if (c->variant == 4)                                                          \
-      hipLaunchKernelGGL((scan_kernel<1, 4, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+      hipLaunchKernelGGL((scan_kernel<2, 4, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+    else if (mode == 2)                                                                \
+      hipLaunchKernelGGL((scan_kernel<2, 0, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
     else if (mode == 1)                                                                \
       hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
     else                                                                               \
@@ -491,18 +506,19 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.pc.overflow = sa.overflow;
   // the carried cut lies in (P - max, P] (its successor needed bytes >= P)
   const uint64_t anchor = (P > cc.origin + p->max) ? P - p->max : cc.origin;
-  const uint64_t seg = std::max<uint64_t>(8 * p->max, 1ull << 20);
+  const uint64_t seg = std::max<uint64_t>(4 * p->max, 1ull << 20);
   const uint64_t end = is_last ? cc.L : P + len;
   const uint64_t nseg = end > anchor ? (end - anchor + seg - 1) / seg : 1;
   ta.anchor = anchor;
   ta.seg = seg;
   ta.nseg = (uint32_t)nseg;
   const double exp_per_seg = (double)seg / (double)p->discriminator + 8.0;
-  uint64_t spg = (uint64_t)((double)kWalkLdsCap / (2.0 * exp_per_seg)) - 1;
-  // the WG's regions (spg+1 segments) must fit one region per thread
-  const uint64_t max_spg_reg = region_bytes ? (200ull * region_bytes) / seg : kMaxSpg;
+  // segments per walk workgroup: about two workgroups per CU (the walks are
+  // latency-bound), within the LDS candidate and region budgets
+  uint64_t spg = std::max<uint64_t>(2, nseg / (2ull * (uint64_t)c->ncu));
+  spg = std::min<uint64_t>(spg, (uint64_t)((double)kWalkLdsCap / (2.0 * exp_per_seg)) - 1);
+  const uint64_t max_spg_reg = region_bytes ? (4000ull * region_bytes) / seg : kMaxSpg;
   spg = std::min<uint64_t>(spg, max_spg_reg > 2 ? max_spg_reg - 2 : 1);
-  spg = std::min<uint64_t>(spg, 32);  // parallelism: >= T/32 walk workgroups
   spg = std::max<uint64_t>(1, std::min<uint64_t>(spg, kMaxSpg));
   ta.spg = (uint32_t)spg;
   ta.lds_cap = kWalkLdsCap;
@@ -978,6 +994,8 @@ extern "C" int dsx_selftest_boundary(dsx_ctx_t* c, const dsx_params_t* p, int mo
   if (!c || !p || !mismatches) return DSX_E_INVAL;
   HIPCHK(c, hipSetDevice(c->device));
   if (mode < 0) mode = pick_mode(c, p->discriminator);
+  const uint32_t d = p->discriminator;
+  if (mode > 2 || (mode == 2 && (d & (d - 1u)) == 0)) return DSX_E_INVAL;  // MODE 2 needs dodd > 1
   DevBuf<unsigned long long> m;
   HIPCHK(c, m.ensure(1));
   HIPCHK(c, hipMemsetAsync(m.p, 0, 8, c->stream));

@@ -36,7 +36,11 @@ struct TestConsts {
   uint32_t qbias;
   uint32_t rot;    // k = ctz(d): rotate right by k
   float rcp;       // fl(1/d)
-  float c0;        // fl(0.5 - (d-1)/d)
+  float c0;        // MODE 1 magic offset 1.5*2^23 - 1
+  uint32_t tadd;   // MODE 2: inv - 1, so t = h*inv + tadd = (h+1)*inv - 1
+  uint32_t vmax;   // MODE 2: 2^k * floor(2^32/d); candidate => t < vmax
+  uint32_t dodd;   // MODE 2: d >> k (h = (t - tadd) * dodd recovers h)
+  uint32_t pad2;
 };
 
 struct ScanArgs {

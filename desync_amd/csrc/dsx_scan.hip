@@ -64,9 +64,25 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t
 //           then the exact check h == q*d + d-1 with a 24-bit mad on those
 //           bits (the constant float offset is folded into tc.madc).
 //           Exact for 1024 < d < 2^22 (DESIGN.md "Boundary test").
+//   MODE 2: t = h*inv + (inv-1) = (h+1)*inv - 1 (mod 2^32); with d = 2^k*dodd
+//           a candidate has h+1 = d*m, so t = 2^k*m - 1 < vmax = 2^k*floor(2^32/d).
+//           For odd d that is exact (multiply back by d); for even d it is a
+//           prefilter with ~2^k/d false positives that mode2_exact re-checks.
+//           The scan accumulates min(t) over 8 bytes and tests once: all
+//           full- or half-rate VALU, no per-byte compare.
+__device__ __forceinline__ uint32_t mode2_t(uint32_t h, const TestConsts& tc) {
+  return h * tc.inv + tc.tadd;
+}
+__device__ __forceinline__ bool mode2_exact(uint32_t t, const TestConsts& tc) {
+  const uint32_t h = (t - tc.tadd) * tc.dodd;  // inv * dodd == 1 (mod 2^32)
+  return t < tc.vmax && h % tc.d == tc.dm1;
+}
+
 template <int MODE>
 __device__ __forceinline__ bool is_cand(uint32_t h, const TestConsts& tc) {
-  if constexpr (MODE == 0) {
+  if constexpr (MODE == 2) {
+    return mode2_exact(mode2_t(h, tc), tc);
+  } else if constexpr (MODE == 0) {
     uint32_t v = (h + 1u) * tc.inv;
     v = __builtin_amdgcn_alignbit(v, v, tc.rot);
     return v - tc.qbias <= tc.qmax;
@@ -85,7 +101,11 @@ __device__ __forceinline__ bool is_cand(uint32_t h, const TestConsts& tc) {
 // reads are in flight, within the 4-bit lgkmcnt).
 // VARIANT (diagnostic ablations; results are wrong for VARIANT != 0):
 // 1 = no boundary test, 3 = staging only (no hashing), 4 = no staging (the
-// kernel hashes whatever the LDS holds: compute ceiling).
+// kernel hashes zeroed LDS staging: compute ceiling).
+// hit entries a lane keeps in registers before spilling to its global slots
+// (a lane segment sees ~S/d hits: 0.2 at 8 KiB and d(64K))
+constexpr int kHitRegs = 4;
+
 template <int SUB>
 __device__ __forceinline__ void lookups_landed(uint64_t (&L)[SUB]) {
   // the empty asm consumes all lookups of a subgroup, so the compiler emits a
@@ -103,8 +123,8 @@ template <bool TEST, int MODE, int VARIANT, int SUB>
 __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t (&ring)[48],
                                         const uint8_t* __restrict__ tbl, uint32_t slot8,
                                         const TestConsts& tc, uint32_t lane, uint32_t obase,
-                                        uint32_t& cnt, uint32_t* __restrict__ myslots,
-                                        uint32_t lane_slots) {
+                                        uint32_t& cnt, uint32_t (&ereg)[kHitRegs],
+                                        uint32_t* __restrict__ myslots, uint32_t lane_slots) {
   if constexpr (VARIANT == 3) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) h ^= w[k];
@@ -124,7 +144,9 @@ __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t
   };
   auto compute = [&](int j) {
     lookups_landed<SUB>(L[j & 1]);
-    uint64_t m[SUB];
+    constexpr bool kTest = TEST && (VARIANT == 0 || VARIANT == 4);
+    uint64_t m[SUB];   // MODE 0/1: per-byte ballots
+    uint32_t t[SUB];   // MODE 2: prefilter values
 #pragma unroll
     for (int i = 0; i < SUB; ++i) {
       const int k = j * SUB + i;
@@ -134,22 +156,38 @@ __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t
       asm("" : "+v"(x));
       h = __builtin_amdgcn_alignbit(h, h, 31) ^ x;
       ring[k] = (uint32_t)(L[j & 1][i] >> 32);
-      if constexpr (TEST && (VARIANT == 0 || VARIANT == 4)) m[i] = __ballot(is_cand<MODE>(h, tc));
+      if constexpr (kTest && MODE == 2) t[i] = mode2_t(h, tc);
+      else if constexpr (kTest) m[i] = __ballot(is_cand<MODE>(h, tc));
     }
-    if constexpr (TEST && VARIANT != 0 && VARIANT != 4) {
+    if constexpr (TEST && !kTest) {
       asm volatile("" ::"v"(h));  // keep the ablated chain live (no DCE)
     } else if constexpr (TEST) {
       // rare path, once per subgroup: a lane with hits appends one entry
       // {hit bits << 16 | offset of the subgroup} (region end expands them)
-      uint64_t any = 0;
+      bool any;
+      if constexpr (MODE == 2) {
+        uint32_t mn = t[0];
 #pragma unroll
-      for (int i = 0; i < SUB; ++i) any |= m[i];
-      if (__builtin_expect(any != 0, 0)) {
+        for (int i = 1; i < SUB; ++i) mn = __builtin_elementwise_min(mn, t[i]);
+        any = __ballot(mn < tc.vmax) != 0;
+      } else {
+        uint64_t a = 0;
+#pragma unroll
+        for (int i = 0; i < SUB; ++i) a |= m[i];
+        any = a != 0;
+      }
+      if (__builtin_expect(any, 0)) {
         uint32_t bits = 0;
 #pragma unroll
-        for (int i = 0; i < SUB; ++i) bits |= (uint32_t)((m[i] >> lane) & 1ull) << i;
+        for (int i = 0; i < SUB; ++i) {
+          if constexpr (MODE == 2) bits |= (mode2_exact(t[i], tc) ? 1u : 0u) << i;
+          else bits |= (uint32_t)((m[i] >> lane) & 1ull) << i;
+        }
         if (bits) {
-          if (cnt < lane_slots) myslots[cnt] = (bits << 16) | (obase + (uint32_t)(j * SUB));
+          const uint32_t e = (bits << 16) | (obase + (uint32_t)(j * SUB));
+#pragma unroll
+          for (int q = 0; q < kHitRegs; ++q) ereg[q] = cnt == (uint32_t)q ? e : ereg[q];
+          if (cnt >= (uint32_t)kHitRegs && cnt - kHitRegs < lane_slots) myslots[cnt - kHitRegs] = e;
           ++cnt;
         }
       }
@@ -193,6 +231,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
       st[4] = 0;             // done, err
       st[5] = 0;             // active, pad
     }
+  }
+  if constexpr (VARIANT == 4) {  // ablation: staging never filled -> zero bytes
+    for (int e = threadIdx.x; e < W * NBUF * STG / 4; e += NT)
+      reinterpret_cast<uint32_t*>(lds + kTableBytes)[e] = 0u;
   }
   // ---- replicate {T, rotl16(T)} over 32 lane slots (64 KiB) ----
   for (int e = threadIdx.x; e < 256 * 32; e += NT) {
@@ -238,49 +280,75 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   asm volatile("" : "+v"(tcv.c0));
   asm volatile("" : "+v"(tcv.madc));
 
-  // regions: the first one per wave statically, then from a work queue (the
+  // Regions: the first one per wave statically, then from a work queue (the
   // two waves sharing a SIMD progress at different rates: VALU arbitration
-  // favours the older one, so static equal shares leave a one-wave tail)
-  uint32_t region = blockIdx.x * W + wave;
-  while (region < a.nregions) {
-    uint32_t next_ticket = 0;
-    if (lane == 0) next_ticket = atomicAdd(a.queue, 1u);  // lands while this region runs
+  // favours the older one, so static equal shares leave a one-wave tail).
+  // The DMA pipeline runs across regions: the last batches of a region issue
+  // the first batches of the next one, so a region start pays no HBM latency.
+  auto desc_of = [&](uint32_t region, u32x4& rsrc, uint32_t& hfix) {
     const uint64_t rbase = (uint64_t)region * 64u * S;  // piece-relative
-    // readable bytes before the region (fewer than 48 only at the chain origin,
-    // where the missing window bytes are virtual zeros: those loads fall out of
-    // the buffer range and return 0)
+    // readable bytes before the region (fewer than 48 only at the chain
+    // origin, where the missing window bytes are virtual zeros: those loads
+    // fall out of the buffer range and return 0)
     const uint32_t H = (rbase + a.halo >= (uint64_t)kRound) ? (uint32_t)kRound
                                                              : (uint32_t)(rbase + a.halo);
     const uint8_t* rptr = a.base + rbase - H;
     const uint64_t nrec64 = a.len - rbase + H;
     const uint32_t nrec = nrec64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nrec64;
     const uint64_t rp = (uint64_t)(uintptr_t)rptr;
-    u32x4 rsrc;
     rsrc.x = __builtin_amdgcn_readfirstlane((uint32_t)rp);
     rsrc.y = __builtin_amdgcn_readfirstlane((uint32_t)(rp >> 32) & 0xFFFFu);  // stride 0
     rsrc.z = __builtin_amdgcn_readfirstlane(nrec);
     rsrc.w = 0x00020000u;
     // batch b covers lane bytes [b*BB - 48, b*BB + BB - 48): buffer offset
     // row*S + b*BB + chunk*16 + (H - 48) (negative wraps -> out of range -> 0)
-    const uint32_t hfix = H - (uint32_t)kRound;
-    auto issue = [&](uint32_t b) {
-      if constexpr (VARIANT == 4) return;  // ablation: hash stale LDS, no HBM traffic
-      const uint32_t dst = stage_lds + (b % NBUF) * (uint32_t)STG;
+    hfix = H - (uint32_t)kRound;
+  };
+  // one batch of DMA into staging slot `slot`; b >= NB issues out-of-range
+  // (zero) loads so that every batch is NI instructions for vmcnt counting
+  auto issue = [&](const u32x4& rsrc, uint32_t hfix, uint32_t b, uint32_t slot) {
+    if constexpr (VARIANT == 4) return;  // ablation: hash stale LDS, no HBM traffic
+    const uint32_t dst = stage_lds + slot * (uint32_t)STG;
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const uint32_t vo = (b < NB) ? dma_off[i] + b * (uint32_t)BB + hfix : 0xFFFFFFF0u;
-        dma16(rsrc, vo, dst + (uint32_t)i * 1024u);
-      }
-    };
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t vo = (b < NB) ? dma_off[i] + b * (uint32_t)BB + hfix : 0xFFFFFFF0u;
+      dma16(rsrc, vo, dst + (uint32_t)i * 1024u);
+    }
+  };
+
+  uint32_t region = blockIdx.x * W + wave;
+  if (region >= a.nregions) return;
+  u32x4 rsrc;
+  uint32_t hfix;
+  desc_of(region, rsrc, hfix);
+  uint32_t gb = 0;  // batches consumed by this wave (staging slot = gb % NBUF)
+  // queue tickets run one region ahead: the ticket naming the successor of
+  // region R is drawn when R-1 starts and read when R starts, where the
+  // implied vmcnt(0) only waits for R's first batches, issued a batch or two
+  // of hashing earlier
+  uint32_t ticket = 0;
+  if (lane == 0) ticket = atomicAdd(a.queue, 1u);
+#pragma unroll
+  for (int q = 0; q < NBUF; ++q) issue(rsrc, hfix, (uint32_t)q, (uint32_t)q);
+
+  while (true) {
+    const uint32_t next = gridDim.x * W + __builtin_amdgcn_readfirstlane(ticket);
+    u32x4 nrsrc = rsrc;
+    uint32_t nhfix = 0;
+    if (next < a.nregions) {
+      if (lane == 0) ticket = atomicAdd(a.queue, 1u);
+      desc_of(next, nrsrc, nhfix);
+    }
 
     // lane state
-    const uint64_t lane_rel = rbase + (uint64_t)lane * S;  // piece-relative lane base
+    const uint64_t lane_rel = (uint64_t)region * 64u * S + (uint64_t)lane * S;
     uint32_t seg_valid = 0;  // offsets o (p = lane base + o) must stay in the piece
     if (lane_rel < a.len) {
       const uint64_t rem = a.len - lane_rel;
       seg_valid = rem < S ? (uint32_t)rem : S;
     }
     uint32_t cnt = 0;
+    uint32_t ereg[kHitRegs] = {};
     const uint64_t gl = (uint64_t)region * 64u + lane;
     uint32_t* myslots = a.lane_slot + gl * a.lane_slots;
 
@@ -289,8 +357,6 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
 #pragma unroll
     for (int k = 0; k < 48; ++k) ring[k] = 0;
 
-#pragma unroll
-    for (int q = 0; q < NBUF; ++q) issue((uint32_t)q);
     // one batch; the warm-up round (window fill, no test) is peeled into the
     // first batch so the steady-state loop has no branch around the rounds
     // (a branch lets the compiler hoist all of a round's table addresses)
@@ -301,7 +367,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
       } else {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (NBUF - 1)) : "memory");
       }
-      const uint8_t* my_row = stage + (b % NBUF) * STG + lane * (uint32_t)BB;
+      const uint32_t slot = NBUF == 1 ? 0u : gb % NBUF;
+      const uint8_t* my_row = stage + slot * STG + lane * (uint32_t)BB;
       uint32_t w[BR * 12];  // BR rounds x 12 dwords
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -314,37 +381,48 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
         w[4 * c + 3] = q.w;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue(b + NBUF);  // refill the buffer just copied; lands during hashing
+      // refill the slot just copied (lands during hashing): this region's
+      // batch b+NBUF, or the next region's first batches
+      if (b + NBUF < NB)
+        issue(rsrc, hfix, b + NBUF, slot);
+      else
+        issue(nrsrc, nhfix, next < a.nregions ? b + NBUF - NB : NB, slot);
+      ++gb;
 #pragma unroll
       for (int r = 0; r < BR; ++r) {
         if (decltype(first)::value && r == 0) {
-          round48<false, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane, 0u, cnt, myslots, 0u);
+          round48<false, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane, 0u, cnt, ereg,
+                                             myslots, 0u);
         } else {
           const uint32_t ri = b * (uint32_t)BR + (uint32_t)r - 1u;  // round index
-          round48<true, MODE, VARIANT, SUB>(w + 12 * r, h, ring, lds, slot8, tcv, lane, ri * 48u, cnt,
-                                       myslots, a.lane_slots);
+          round48<true, MODE, VARIANT, SUB>(w + 12 * r, h, ring, lds, slot8, tcv, lane, ri * 48u,
+                                            cnt, ereg, myslots, a.lane_slots);
         }
       }
     };
     batch(0u, std::true_type{});
     for (uint32_t b = 1; b < NB; ++b) batch(b, std::false_type{});
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // ---- region end: compact the lanes' hits into one sorted region list ----
-    // (slots were written by this lane in the rare path; candidates before
+    // (entries were written by this lane in the rare path; candidates before
     // min_pos -- windows reaching before the chain origin -- are dropped)
     const uint64_t lane_abs = a.piece_abs + lane_rel;
     const uint32_t o_min = lane_abs >= a.min_pos ? 0u : (uint32_t)(a.min_pos - lane_abs);
-    const uint32_t n = cnt < a.lane_slots ? cnt : a.lane_slots;
+    const uint32_t n = cnt < a.lane_slots + kHitRegs ? cnt : a.lane_slots + kHitRegs;
+    const bool spilled = __ballot(cnt > (uint32_t)kHitRegs) != 0;  // rare: global reads
     auto for_each_hit = [&](auto&& f) {
-      for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t e = myslots[i];
+      auto expand = [&](uint32_t e) {
         const uint32_t base = e & 0xFFFFu;
         for (uint32_t bits = e >> 16; bits; bits &= bits - 1u) {
           const uint32_t o = base + (uint32_t)__builtin_ctz(bits) + 1u;  // offset in lane seg
           if (o >= o_min && o <= seg_valid) f(o);
         }
-      }
+      };
+#pragma unroll
+      for (int q = 0; q < kHitRegs; ++q)
+        if ((uint32_t)q < n) expand(ereg[q]);
+      if (spilled)
+        for (uint32_t i = kHitRegs; i < n; ++i) expand(myslots[i - kHitRegs]);
     };
     uint32_t keep = 0;
     for_each_hit([&](uint32_t) { ++keep; });
@@ -364,21 +442,26 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
       if (excl + j < a.region_cap) rl[excl + j] = lane * S + o;
       ++j;
     });
-    const bool lane_ovf = __ballot(cnt > a.lane_slots) != 0;
+    const bool lane_ovf = __ballot(cnt > a.lane_slots + kHitRegs) != 0;
     if (lane == 0) {
       a.region_cnt[region] = exact;
       if (lane_ovf || exact > a.region_cap) atomicAdd(a.overflow, 1u);
     }
-    region = gridDim.x * W + __builtin_amdgcn_readfirstlane(next_ticket);
+    if (next >= a.nregions) break;
+    region = next;
+    rsrc = nrsrc;
+    hfix = nhfix;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the trailing zero loads
 }
 
 #define DSX_SCAN_INST(BR, NBUF, W, SUB)                                   \
   template __global__ void scan_kernel<0, 0, BR, NBUF, W, SUB>(ScanArgs); \
   template __global__ void scan_kernel<1, 0, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<1, 1, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<1, 3, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<1, 4, BR, NBUF, W, SUB>(ScanArgs);
+  template __global__ void scan_kernel<2, 0, BR, NBUF, W, SUB>(ScanArgs); \
+  template __global__ void scan_kernel<2, 1, BR, NBUF, W, SUB>(ScanArgs); \
+  template __global__ void scan_kernel<2, 3, BR, NBUF, W, SUB>(ScanArgs); \
+  template __global__ void scan_kernel<2, 4, BR, NBUF, W, SUB>(ScanArgs);
 DSX_SCAN_INST(2, 2, 8, 8)
 DSX_SCAN_INST(1, 2, 12, 4)
 DSX_SCAN_INST(1, 2, 16, 4)
@@ -392,7 +475,7 @@ __global__ void boundary_selftest_kernel(TestConsts tc, int mode, uint64_t h0, u
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t h = (uint32_t)(h0 + i);
     const bool want = (h % tc.d) == tc.dm1;
-    const bool got = mode == 1 ? is_cand<1>(h, tc) : is_cand<0>(h, tc);
+    const bool got = mode == 2 ? is_cand<2>(h, tc) : (mode == 1 ? is_cand<1>(h, tc) : is_cand<0>(h, tc));
     bad += (want != got);
   }
   if (bad) atomicAdd(mismatches, bad);

@@ -116,13 +116,38 @@ __device__ __forceinline__ uint64_t seg_end(const StitchArgs& a, uint32_t k) {
 
 // ---- K2: per-segment speculative walks ------------------------------------
 constexpr int kWalkThreads = 256;
+constexpr uint32_t kWalkMaxRegions = 4096;  // regions a walk workgroup can stage
+
+// Block-wide exclusive scan of one value per thread (kWalkThreads threads);
+// returns the exclusive prefix, *total gets the block sum.
+__device__ uint32_t walk_block_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += t;
+  }
+  if (lane == 63) s_wave[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < kWalkThreads / 64; ++i) {
+    const uint32_t t = s_wave[i];
+    before += (i < (int)wv) ? t : 0u;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
 
 __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* cand = smem;                         // [a.lds_cap]
   uint64_t* xs = (uint64_t*)(smem + a.lds_cap);  // [kMaxSpg + 1] spec exits
-  __shared__ uint32_t s_part[kWalkThreads];
-  __shared__ uint32_t s_total;
+  __shared__ uint32_t s_off[kWalkMaxRegions + 1];
+  __shared__ uint32_t s_wave[kWalkThreads / 64];
 
   const DevState* st = a.state;
   if (st->done || *a.pc.overflow) return;  // finished, or scan lists overflowed
@@ -140,35 +165,38 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   uint64_t r1 = hi <= pc.P ? 0 : (hi - pc.P - 1) / pc.RB + 1;  // exclusive
   if (r1 > pc.nregions) r1 = pc.nregions;
   const uint32_t nreg = r1 > r0 ? (uint32_t)(r1 - r0) : 0u;
-  bool dense = nreg > kWalkThreads;
-  if (!dense && threadIdx.x < nreg) {
-    const uint32_t c = pc.region_cnt[r0 + threadIdx.x];
-    s_part[threadIdx.x] = c < pc.region_cap ? c : pc.region_cap;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {  // tiny serial scan over the WG's regions
-    uint32_t acc = 0;
-    for (uint32_t i = 0; i < nreg && i < kWalkThreads; ++i) {
-      const uint32_t v = s_part[i];
-      s_part[i] = acc;
-      acc += v;
+  bool dense = nreg > kWalkMaxRegions;
+  uint32_t total = 0;
+  if (!dense) {
+    // region counts -> exclusive offsets s_off[0..nreg]
+    for (uint32_t b = 0; b < nreg; b += kWalkThreads) {
+      const uint32_t i = b + threadIdx.x;
+      uint32_t c = 0;
+      if (i < nreg) {
+        c = pc.region_cnt[r0 + i];
+        c = c < pc.region_cap ? c : pc.region_cap;
+      }
+      uint32_t part;
+      const uint32_t ex = walk_block_scan(c, s_wave, &part);
+      if (i < nreg) s_off[i] = total + ex;
+      total += part;
     }
-    s_total = acc;
+    if (threadIdx.x == 0) s_off[nreg] = total;
+    __syncthreads();
+    dense = total > a.lds_cap;
   }
-  __syncthreads();
-  const uint32_t total = s_total;
-  dense = dense || total > a.lds_cap;
-  if (!dense && threadIdx.x < nreg) {
-    const uint64_t r = r0 + threadIdx.x;
-    const uint32_t c = pc.region_cnt[r];
-    const uint32_t n = c < pc.region_cap ? c : pc.region_cap;
-    const uint64_t base = pc.P + r * pc.RB;
-    const uint32_t* l = pc.region_list + r * (uint64_t)pc.region_cap;
-    uint32_t o = s_part[threadIdx.x];
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint64_t p = base + l[i];
+  if (!dense) {
+    // one candidate per thread: find its region by binary search over s_off
+    for (uint32_t g = threadIdx.x; g < total; g += kWalkThreads) {
+      uint32_t l = 0, h = nreg;  // last r with s_off[r] <= g
+      while (h - l > 1) {
+        const uint32_t m = (l + h) >> 1;
+        if (s_off[m] <= g) l = m; else h = m;
+      }
+      const uint64_t r = r0 + l;
+      const uint64_t p = pc.P + r * pc.RB + pc.region_list[r * (uint64_t)pc.region_cap + (g - s_off[l])];
       // keep the array sorted: below-range -> 0, above-range -> UINT32_MAX
-      cand[o++] = p <= lo ? 0u : (p > hi ? 0xFFFFFFFFu : (uint32_t)(p - lo));
+      cand[g] = p <= lo ? 0u : (p > hi ? 0xFFFFFFFFu : (uint32_t)(p - lo));
     }
   }
   __syncthreads();

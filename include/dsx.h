@@ -170,7 +170,8 @@ int dsx_shard_resolve(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, int ran
 
 /* ---- diagnostics ------------------------------------------------------------- */
 /* Evaluates the GPU boundary predicate (mode 0: multiply-inverse form of
- * chunker.go:265, mode 1: float-reciprocal form, -1: the one the scan uses)
+ * chunker.go:265, mode 1: float-reciprocal form, mode 2: multiply-inverse
+ * prefilter + exact re-check (d not a power of two), -1: the one the scan uses)
  * for h in [h0, h0+n) (mod 2^32) against h % d == d-1 and counts mismatches
  * (the check of chunker_test.go:190-213, on the device). */
 int dsx_selftest_boundary(dsx_ctx_t *ctx, const dsx_params_t *p, int mode, uint64_t h0,

@@ -34,7 +34,7 @@ def gpu_cut(dctx, arr, mn=MIN, av=AVG, mx=MAX):
 
 # ---------------------------------------------------------------- predicate
 @pytest.mark.parametrize("avg", [16 * 1024, 64 * 1024, 256 * 1024, 1024 * 1024, 8192, 4096, 1000])
-@pytest.mark.parametrize("mode", [0, 1, -1])
+@pytest.mark.parametrize("mode", [0, 1, 2, -1])
 def test_boundary_predicate_ranges(dctx, avg, mode):
     """chunker_test.go:190-213 on the device: [0,3d) and [2^32-1-3d, 2^32)."""
     import desync_amd
@@ -43,7 +43,9 @@ def test_boundary_predicate_ranges(dctx, avg, mode):
     d = p.discriminator
     if mode == 1 and not (2048 < d < (1 << 24)):
         pytest.skip("float form is only used for 2048 < d < 2^24")
-    for h0, n in ((0, 3 * d), (2**32 - 1 - 3 * d, 3 * d + 1)):
+    if mode == 2 and d & (d - 1) == 0:
+        pytest.skip("prefilter form needs d with an odd factor > 1")
+    for h0, n in ((0, 3 * d), (2**32 - 1 - 3 * d, 3 * d + 1), (0x5A5A5A5A, 1 << 24)):
         bad = ctypes.c_uint64()
         _lib.check(_lib.lib().dsx_selftest_boundary(dctx.h, ctypes.byref(p.c), mode, h0, n,
                                                     ctypes.byref(bad)), dctx.h)
@@ -51,13 +53,14 @@ def test_boundary_predicate_ranges(dctx, avg, mode):
 
 
 @pytest.mark.parametrize("avg", [16 * 1024, 64 * 1024, 256 * 1024])
-def test_boundary_predicate_exhaustive(dctx, avg):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_boundary_predicate_exhaustive(dctx, avg, mode):
     """All 2^32 hash values for the BASELINE discriminators."""
     import desync_amd
     from desync_amd import _lib
     p = desync_amd.Params(avg // 4, avg, avg * 4)
     bad = ctypes.c_uint64()
-    _lib.check(_lib.lib().dsx_selftest_boundary(dctx.h, ctypes.byref(p.c), -1, 0, 1 << 32,
+    _lib.check(_lib.lib().dsx_selftest_boundary(dctx.h, ctypes.byref(p.c), mode, 0, 1 << 32,
                                                 ctypes.byref(bad)), dctx.h)
     assert bad.value == 0
 

@@ -1,9 +1,9 @@
 #!/bin/bash
-# regions-per-slot sweep for the scan work queue
+# regions-per-slot x variant sweep for one scan config (CFG, default 0)
 set -o pipefail
-timeout -k 10 400 python -m pytest tests -m gpu -x -q -k "not config2 and not config4 and not host_and_fd and not exhaustive" > gpurun_out/q_tests.log 2>&1 || { tail -30 gpurun_out/q_tests.log; exit 1; }
-tail -1 gpurun_out/q_tests.log
-for r in 1 2 4 8; do
-  o=$(DSX_REGIONS_PER_SLOT=$r timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu 2>/dev/null | grep -o '"kernel_ms": [0-9.]*\|"value": [0-9.]*\|"stitch_ms": [0-9.]*' | tr '\n' ' ') || exit 1
-  echo "rps=$r $o"
+for r in ${RPS:-1 4}; do
+for v in ${VARS:-0 3 4}; do
+  o=$(DSX_SCAN_CFG=${CFG:-0} DSX_SCAN_VARIANT=$v DSX_REGIONS_PER_SLOT=$r timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu 2>/dev/null | grep -o '"kernel_ms": [0-9.]*\|"value": [0-9.]*\|"stitch_ms": [0-9.]*' | tr '\n' ' ') || exit 1
+  echo "cfg=${CFG:-0} rps=$r variant=$v $o"
+done
 done

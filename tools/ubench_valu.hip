@@ -1,0 +1,139 @@
+// ubench_valu.hip -- VALU issue throughput per instruction type on gfx950
+// (standalone microbenchmark, tools/, not part of libdsx).  Each kernel runs
+// ITER iterations of 8 independent inline-asm instructions per lane; prints
+// wave64 instructions per SIMD per cycle (from wall time and the clock).
+//   hipcc --offload-arch=gfx950 -O3 tools/ubench_valu.hip -o tools/ubench_valu
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+constexpr int ITER = 4096;
+
+#define BODY8(INS)                                                                  \
+  asm volatile(INS : "+v"(a0) : "v"(b), "v"(c)); asm volatile(INS : "+v"(a1) : "v"(b), "v"(c)); \
+  asm volatile(INS : "+v"(a2) : "v"(b), "v"(c)); asm volatile(INS : "+v"(a3) : "v"(b), "v"(c)); \
+  asm volatile(INS : "+v"(a4) : "v"(b), "v"(c)); asm volatile(INS : "+v"(a5) : "v"(b), "v"(c)); \
+  asm volatile(INS : "+v"(a6) : "v"(b), "v"(c)); asm volatile(INS : "+v"(a7) : "v"(b), "v"(c));
+
+#define KERNEL(NAME, INS)                                                            \
+  __global__ void NAME(uint32_t* out, uint32_t seed) {                              \
+    uint32_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, \
+             a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;                                  \
+    uint32_t b = seed * 3u + 1u, c = seed * 5u + 7u;                                 \
+    for (int i = 0; i < ITER; ++i) { BODY8(INS) }                                   \
+    uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;                              \
+    if (r == 0x12345679u) out[0] = r;                                               \
+  }
+
+KERNEL(k_xor, "v_xor_b32 %0, %0, %1")
+KERNEL(k_add, "v_add_u32 %0, %0, %1")
+KERNEL(k_alignbit, "v_alignbit_b32 %0, %0, %0, 31")
+KERNEL(k_perm, "v_perm_b32 %0, %0, %1, %2")
+KERNEL(k_cvt, "v_cvt_f32_u32 %0, %0")
+KERNEL(k_fma, "v_fma_f32 %0, %0, %1, %2")
+KERNEL(k_mul_f32, "v_mul_f32 %0, %0, %1")
+KERNEL(k_mad24, "v_mad_u32_u24 %0, %0, %1, %2")
+KERNEL(k_mul24, "v_mul_u32_u24 %0, %0, %1")
+KERNEL(k_xad, "v_xad_u32 %0, %0, %1, %2")
+KERNEL(k_or3, "v_or3_b32 %0, %0, %1, %2")
+KERNEL(k_lshl_or, "v_lshl_or_b32 %0, %0, 1, %1")
+KERNEL(k_bfi, "v_bfi_b32 %0, %0, %1, %2")
+KERNEL(k_min3, "v_min3_u32 %0, %0, %1, %2")
+KERNEL(k_sad, "v_sad_u32 %0, %0, %1, %2")
+KERNEL(k_mullo, "v_mul_lo_u32 %0, %0, %1")
+KERNEL(k_mulhi, "v_mul_hi_u32 %0, %0, %1")
+KERNEL(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
+KERNEL(k_sdwa_mov, "v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2")
+KERNEL(k_sdwa_or, "v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2")
+KERNEL(k_min, "v_min_u32 %0, %0, %1")
+KERNEL(k_sub, "v_sub_u32 %0, %0, %1")
+KERNEL(k_lshr, "v_lshrrev_b32 %0, 3, %0")
+KERNEL(k_and, "v_and_b32 %0, %0, %1")
+KERNEL(k_cvt_ubyte, "v_cvt_f32_ubyte1 %0, %0")
+
+// compare into SGPR pairs + s_or accumulate (ballot pattern)
+__global__ void k_cmp(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+  uint32_t b = seed * 3u + 1u;
+  uint64_t acc = 0;
+  for (int i = 0; i < ITER; ++i) {
+    uint64_t m0, m1, m2, m3;
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m0) : "v"(a0), "v"(b));
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m1) : "v"(a1), "v"(b));
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m2) : "v"(a2), "v"(b));
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m3) : "v"(a3), "v"(b));
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m0) : "v"(a0), "v"(a1));
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m1) : "v"(a1), "v"(a2));
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m2) : "v"(a2), "v"(a3));
+    asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m3) : "v"(a3), "v"(a0));
+    acc |= m0 | m1 | m2 | m3;
+  }
+  if (acc == 0x12345679u) out[0] = (uint32_t)acc;
+}
+
+// packed f32 fma (2 lanes of work per instruction)
+__global__ void k_pkfma(uint32_t* out, uint32_t seed) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 a0 = {(float)threadIdx.x, 1.f}, a1 = a0 + 1.f, a2 = a0 + 2.f, a3 = a0 + 3.f, a4 = a0 + 4.f,
+     a5 = a0 + 5.f, a6 = a0 + 6.f, a7 = a0 + 7.f;
+  f2 b = {1.0001f, 0.9999f}, c = {0.5f, 0.25f};
+  for (int i = 0; i < ITER; ++i) { BODY8("v_pk_fma_f32 %0, %0, %1, %2") }
+  f2 r = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+  if (r.x == 1234.5f) out[0] = 1;
+}
+
+// dependent chain: alignbit -> xor (the hash recurrence), 8 chains interleaved
+__global__ void k_chain(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+           a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t b = seed * 3u + 1u, c = 0;
+  for (int i = 0; i < ITER / 2; ++i) {
+    BODY8("v_alignbit_b32 %0, %0, %0, 31")
+    BODY8("v_xor_b32 %0, %0, %1")
+  }
+  uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+  if (r == 0x12345679u + c) out[0] = r;
+}
+
+int main() {
+  uint32_t* o;
+  CHK(hipMalloc(&o, 64));
+  int clk_khz = 0;
+  CHK(hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0));
+  const int ncu = 256;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  struct K { const char* name; void (*f)(uint32_t*, uint32_t); int per_iter; };
+  K ks[] = {{"v_xor_b32", k_xor, 8},       {"v_xor_b32_e64", k_xor_e64, 8}, {"v_add_u32", k_add, 8},
+            {"v_alignbit_b32", k_alignbit, 8}, {"v_perm_b32", k_perm, 8},   {"v_cvt_f32_u32", k_cvt, 8},
+            {"v_fma_f32", k_fma, 8},       {"v_mul_f32", k_mul_f32, 8},     {"v_mad_u32_u24", k_mad24, 8},
+            {"v_mul_u32_u24", k_mul24, 8}, {"v_xad_u32", k_xad, 8},         {"v_or3_b32", k_or3, 8},
+            {"v_lshl_or_b32", k_lshl_or, 8}, {"v_bfi_b32", k_bfi, 8},       {"v_min3_u32", k_min3, 8},
+            {"v_sad_u32", k_sad, 8},       {"v_mul_lo_u32", k_mullo, 8},    {"v_mul_hi_u32", k_mulhi, 8},
+            {"v_cmp_e64+s_or", k_cmp, 8},  {"v_mov_b32_sdwa", k_sdwa_mov, 8}, {"v_or_b32_sdwa", k_sdwa_or, 8},
+            {"v_min_u32", k_min, 8},       {"v_sub_u32", k_sub, 8},         {"v_lshrrev_b32", k_lshr, 8},
+            {"v_and_b32", k_and, 8},       {"v_cvt_f32_ubyte1", k_cvt_ubyte, 8},  {"v_pk_fma_f32", k_pkfma, 8},    {"chain alignbit+xor", k_chain, 8}};
+  printf("clock attr %d kHz\n", clk_khz);
+  for (int wps : {2}) {
+    for (auto& k : ks) {
+      const int threads = 64 * 4 * wps;  // one block per CU, wps waves per SIMD
+      hipLaunchKernelGGL(k.f, dim3(ncu), dim3(threads), 0, 0, o, 1u);
+      hipEventRecord(e0);
+      const int reps = 5;
+      for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k.f, dim3(ncu), dim3(threads), 0, 0, o, 1u);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      ms /= reps;
+      // wave64 instructions per SIMD: wps waves x ITER x per_iter
+      const double inst = (double)wps * ITER * k.per_iter;
+      const double cyc = ms * 1e-3 * clk_khz * 1e3;
+      printf("wps=%d %-22s %8.3f ms  %.3f cyc/inst/SIMD\n", wps, k.name, ms, cyc / inst);
+    }
+  }
+  return 0;
+}
