@@ -16,12 +16,12 @@ from .chunker import ChunkerWindowSize, Chunker, NewChunker, Params  # noqa: F40
 from .digest import SHA256, SHA512256, NewNullChunk, NullChunk, set_digest  # noqa: F401
 from .errors import Interrupted  # noqa: F401
 from .index import FormatIndex, Index, IndexChunk, IndexFromReader  # noqa: F401
-from .make import ChunkingStats, IndexFromFile, cut_device, cut_device_result, cut_fd, \
-    cut_host  # noqa: F401
+from .make import ChunkingStats, IndexFromFile, chunk_ids, cut_device, cut_device_result, \
+    cut_fd, cut_host  # noqa: F401
 
 __all__ = [
     "ChunkerWindowSize", "Chunker", "NewChunker", "Params", "SHA256", "SHA512256", "NullChunk",
     "NewNullChunk", "set_digest", "Interrupted", "FormatIndex", "Index", "IndexChunk",
     "IndexFromReader", "ChunkingStats", "IndexFromFile", "cut_device", "cut_device_result",
-    "cut_fd", "cut_host",
+    "cut_fd", "cut_host", "chunk_ids",
 ]

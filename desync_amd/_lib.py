@@ -42,8 +42,12 @@ EXPORTS = (
     "dsx_last_error", "dsx_cancel", "dsx_cut_device", "dsx_sync", "dsx_result", "dsx_cut_host",
     "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
     "dsx_stream_done", "dsx_stream_chunk_data", "dsx_shard_local", "dsx_shard_resolve",
-    "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_get_stats",
+    "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
+    "dsx_get_stats",
 )
+DSX_DIGEST_SHA512_256 = 0
+DSX_DIGEST_SHA256 = 1
+DSX_ENDS_DEVICE = 4
 
 
 class Params(ctypes.Structure):
@@ -133,6 +137,7 @@ def lib():
             "dsx_selftest_boundary": (i32, [vp, P(Params), i32, u64, u64, P(u64)]),
             "dsx_gen_uniform": (i32, [vp, vp, u64, u64, u64]),
             "dsx_gen_dedup": (i32, [vp, vp, u64, u64, u64, ctypes.c_double]),
+            "dsx_chunk_ids": (i32, [vp, vp, u64, u64, vp, u64, vp, u32, i32]),
             "dsx_get_stats": (i32, [vp, P(Stats)]),
         }
         for name, (res, args) in sig.items():

@@ -22,10 +22,13 @@
 
 #include "../../include/dsx.h"
 #include "dsx_common.h"
+#include "dsx_digest.h"
 #include "dsx_stitch.h"
 
 namespace dsx {
-template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB>
+template <class H>
+__global__ void digest_kernel(DigestArgs a);
+template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ void scan_kernel(ScanArgs a);
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
@@ -87,13 +90,17 @@ struct dsx_ctx {
   int force_mode = -1;  // DSX_TEST_MODE env override
   int variant = 0;      // DSX_SCAN_VARIANT: diagnostic scan ablations (wrong results)
   uint32_t lane_bytes_override = 0;  // DSX_LANE_BYTES (tuning; multiple of 48)
-  int regions_per_slot = 4;           // DSX_REGIONS_PER_SLOT: scan work units per wave slot
+  int prefetch_batches = 0;           // DSX_PREFETCH: L2 prefetch distance in DMA batches (0 = off)
+  int regions_per_slot = 1;           // DSX_REGIONS_PER_SLOT: scan work units per wave slot
   int scan_cfg = 0;                   // DSX_SCAN_CFG: 0 = 8 waves x 2 LDS buffers, 1 = 12 x 1, 2 = 16 x 1
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
   DevBuf<uint32_t> lane_slot;
   DevBuf<SegInfo> seg_info;
   DevBuf<uint64_t> stage, rep, out_off, out;
+  DevBuf<uint64_t> dg_ends;   // chunk IDs: staged chunk ends
+  DevBuf<uint8_t> dg_ids;     // chunk IDs: staged digests
+  DevBuf<uint32_t> dg_queue;  // chunk IDs: lane work queue
   DevBuf<DevState> state;
   DevBuf<uint8_t> dbuf[2];
   uint8_t* pinned[2] = {nullptr, nullptr};
@@ -284,6 +291,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   c->ncu = prop.multiProcessorCount;
   if (const char* m = getenv("DSX_TEST_MODE")) c->force_mode = atoi(m);
   if (const char* v = getenv("DSX_SCAN_VARIANT")) c->variant = atoi(v);
+  if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(2, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
@@ -317,6 +325,7 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   c->region_cnt.release(); c->region_list.release(); c->overflow.release(); c->rep_cnt.release(); c->rep_from.release();
   c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
+  c->dg_ends.release(); c->dg_ids.release(); c->dg_queue.release();
   c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
   c->dbuf[0].release(); c->dbuf[1].release();
   for (auto& p : c->pinned) if (p) (void)hipHostFree(p);
@@ -443,6 +452,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   sa.tc = make_tc(p);
   sa.min_pos = cc.min_pos;
   sa.lane_slots = LS;
+  sa.pf_batches = (uint32_t)c->prefetch_batches;
   sa.lane_slot = c->lane_slot.p;
   sa.region_cnt = c->region_cnt.p;
   sa.region_list = c->region_list.p;
@@ -465,27 +475,29 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)c->ncu);
     const dim3 g(grid), b(W * kWave);
     const int mode = pick_mode(c, p->discriminator);
-#define DSX_LAUNCH(BR, NB, WV, SUB)                                                    \
-  do {                                                                                 \
-    if (c->variant == 1)                                                               \
-      hipLaunchKernelGGL((scan_kernel<2, 1, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
-    else if (c->variant == 3)                                                          \
-      hipLaunchKernelGGL((scan_kernel<2, 3, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
-    else if (c->variant == 4)                                                          \
-      hipLaunchKernelGGL((scan_kernel<2, 4, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
-    else if (mode == 2)                                                                \
-      hipLaunchKernelGGL((scan_kernel<2, 0, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
-    else if (mode == 1)                                                                \
-      hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
-    else                                                                               \
-      hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB>), g, b, 0, c->stream, sa); \
+#define DSX_LAUNCH(BR, NB, WV, SUB, PF)                                                    \
+  do {                                                                                     \
+    if (c->variant == 1)                                                                   \
+      hipLaunchKernelGGL((scan_kernel<2, 1, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+    else if (c->variant == 3)                                                              \
+      hipLaunchKernelGGL((scan_kernel<2, 3, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+    else if (c->variant == 4)                                                              \
+      hipLaunchKernelGGL((scan_kernel<2, 4, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+    else if (mode == 2)                                                                    \
+      hipLaunchKernelGGL((scan_kernel<2, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+    else if (mode == 1)                                                                    \
+      hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+    else                                                                                   \
+      hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
   } while (0)
-    if (W == 8)
-      DSX_LAUNCH(2, 2, 8, 8);
+    if (W == 8 && c->prefetch_batches > 0)
+      DSX_LAUNCH(2, 2, 8, 8, true);
+    else if (W == 8)
+      DSX_LAUNCH(2, 2, 8, 8, false);
     else if (W == 12)
-      DSX_LAUNCH(1, 2, 12, 4);
+      DSX_LAUNCH(1, 2, 12, 4, false);
     else
-      DSX_LAUNCH(1, 2, 16, 4);
+      DSX_LAUNCH(1, 2, 16, 4, false);
 #undef DSX_LAUNCH
     HIPCHK(c, hipGetLastError());
   }
@@ -982,6 +994,58 @@ extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_
   hipLaunchKernelGGL(gen_dedup_kernel, dim3(grid), dim3(256), 0, c->stream, (uint8_t*)d_dst,
                      offset, len, seed, thresh);
   HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return DSX_OK;
+}
+
+// --------------------------------------------------------------------------
+// chunk IDs (Digest.Sum per chunk: digest.go:11-29, make.go:223)
+// --------------------------------------------------------------------------
+extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uint64_t start,
+                             const uint64_t* ends, uint64_t n, void* ids, uint32_t flags,
+                             int algo) {
+  if (!c || (n && (!d_blob || !ends || !ids)) || (algo != DSX_DIGEST_SHA512_256 &&
+                                                   algo != DSX_DIGEST_SHA256))
+    return DSX_E_INVAL;
+  if ((flags & ~(DSX_OUT_DEVICE | DSX_ENDS_DEVICE)) != 0) return DSX_E_INVAL;
+  if (n == 0) return DSX_OK;
+  if (n > 0xFFFFFFF0ull) return DSX_E_INVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  c->err.clear();
+  const uint64_t* d_ends = ends;
+  if (!(flags & DSX_ENDS_DEVICE)) {
+    HIPCHK(c, grow(c, c->dg_ends, n));
+    HIPCHK(c, hipMemcpyAsync(c->dg_ends.p, ends, n * 8, hipMemcpyHostToDevice, c->stream));
+    d_ends = c->dg_ends.p;
+  }
+  uint8_t* d_ids = (uint8_t*)ids;
+  if (!(flags & DSX_OUT_DEVICE)) {
+    HIPCHK(c, grow(c, c->dg_ids, n * 32));
+    d_ids = c->dg_ids.p;
+  }
+  HIPCHK(c, c->dg_queue.ensure(1));
+  HIPCHK(c, hipMemsetAsync(c->dg_queue.p, 0, 4, c->stream));
+  // lanes: up to 4 workgroups of 256 per CU, each lane pulls chunks from the queue
+  const uint64_t blocks = std::min<uint64_t>((n + kDigestThreads - 1) / kDigestThreads,
+                                             4ull * (uint64_t)c->ncu);
+  DigestArgs da{};
+  da.blob = (const uint8_t*)d_blob;
+  da.len = len;
+  da.ends = d_ends;
+  da.first_start = start;
+  da.n = n;
+  da.ids = d_ids;
+  da.queue = c->dg_queue.p;
+  da.nfirst = (uint32_t)std::min<uint64_t>(n, blocks * kDigestThreads);
+  if (algo == DSX_DIGEST_SHA512_256)
+    hipLaunchKernelGGL(digest_kernel<Sha512>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
+                       c->stream, da);
+  else
+    hipLaunchKernelGGL(digest_kernel<Sha256>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
+                       c->stream, da);
+  HIPCHK(c, hipGetLastError());
+  if (!(flags & DSX_OUT_DEVICE))
+    HIPCHK(c, hipMemcpyAsync(ids, d_ids, n * 32, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return DSX_OK;
 }

@@ -55,7 +55,7 @@ struct ScanArgs {
   TestConsts tc;
   uint64_t min_pos;      // candidates at absolute p < min_pos are dropped (origin + 49)
   uint32_t lane_slots;   // slot capacity per lane (kLaneSlots, or S on the dense path)
-  uint32_t pad2;
+  uint32_t pf_batches;   // L2 prefetch distance in batches (PF kernels only)
   uint32_t* lane_slot;   // scratch [nregions*64*lane_slots]: per-lane hit entries (rare writes)
   uint32_t* region_cnt;  // [nregions] candidates per region (exact)
   uint32_t* region_list; // [nregions*region_cap] sorted offsets in (0, 64*S] from region base

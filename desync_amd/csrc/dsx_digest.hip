@@ -1,0 +1,295 @@
+// dsx_digest.hip -- chunk IDs on the GPU: SHA-512/256 (desync's default
+// Digest, digest.go:11-22, crypto/sha512.Sum512_256) and SHA-256 (the
+// --digest sha256 alternative, digest.go:24-29), one digest per chunk
+// [ends[i-1], ends[i]) of a device-resident blob (IndexChunk.ID, make.go:223).
+//
+// SHA-2 over one chunk is a sequential chain of block compressions, so the
+// parallelism is one chunk per lane.  Chunk sizes vary 16x (min..max), so a
+// static chunk-per-lane split would leave most lanes of a wave idle behind its
+// longest chunk: lanes instead pull chunks from a global queue the moment they
+// finish one (one atomic per wave per refill, prefix by mbcnt), and every
+// loop iteration compresses one block on every live lane.  A chunk's last one
+// or two blocks (the padded tail, FIPS 180-4 sec.5.1) are assembled byte-wise
+// with explicit bounds; full blocks come from aligned 16-byte loads
+// re-aligned with v_alignbyte.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dsx_digest.h"
+
+namespace dsx {
+
+// ---- SHA-512 constants (FIPS 180-4 sec.4.2.3, sec.5.3.6.2 for the /256 IV) --
+__constant__ uint64_t kK512[80] = {
+    0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
+    0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
+    0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
+    0x72be5d74f27b896full, 0x80deb1fe3b1696b1ull, 0x9bdc06a725c71235ull, 0xc19bf174cf692694ull,
+    0xe49b69c19ef14ad2ull, 0xefbe4786384f25e3ull, 0x0fc19dc68b8cd5b5ull, 0x240ca1cc77ac9c65ull,
+    0x2de92c6f592b0275ull, 0x4a7484aa6ea6e483ull, 0x5cb0a9dcbd41fbd4ull, 0x76f988da831153b5ull,
+    0x983e5152ee66dfabull, 0xa831c66d2db43210ull, 0xb00327c898fb213full, 0xbf597fc7beef0ee4ull,
+    0xc6e00bf33da88fc2ull, 0xd5a79147930aa725ull, 0x06ca6351e003826full, 0x142929670a0e6e70ull,
+    0x27b70a8546d22ffcull, 0x2e1b21385c26c926ull, 0x4d2c6dfc5ac42aedull, 0x53380d139d95b3dfull,
+    0x650a73548baf63deull, 0x766a0abb3c77b2a8ull, 0x81c2c92e47edaee6ull, 0x92722c851482353bull,
+    0xa2bfe8a14cf10364ull, 0xa81a664bbc423001ull, 0xc24b8b70d0f89791ull, 0xc76c51a30654be30ull,
+    0xd192e819d6ef5218ull, 0xd69906245565a910ull, 0xf40e35855771202aull, 0x106aa07032bbd1b8ull,
+    0x19a4c116b8d2d0c8ull, 0x1e376c085141ab53ull, 0x2748774cdf8eeb99ull, 0x34b0bcb5e19b48a8ull,
+    0x391c0cb3c5c95a63ull, 0x4ed8aa4ae3418acbull, 0x5b9cca4f7763e373ull, 0x682e6ff3d6b2b8a3ull,
+    0x748f82ee5defb2fcull, 0x78a5636f43172f60ull, 0x84c87814a1f0ab72ull, 0x8cc702081a6439ecull,
+    0x90befffa23631e28ull, 0xa4506cebde82bde9ull, 0xbef9a3f7b2c67915ull, 0xc67178f2e372532bull,
+    0xca273eceea26619cull, 0xd186b8c721c0c207ull, 0xeada7dd6cde0eb1eull, 0xf57d4f7fee6ed178ull,
+    0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
+    0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
+    0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
+__constant__ uint64_t kIV512_256[8] = {
+    0x22312194fc2bf72cull, 0x9f555fa3c84c64c2ull, 0x2393b86b6f53b151ull, 0x963877195940eabdull,
+    0x96283ee2a88effe3ull, 0xbe5e1e2553863992ull, 0x2b0199fc2c85b8aaull, 0x0eb72ddc81c52ca2ull};
+
+// ---- SHA-256 constants (FIPS 180-4 sec.4.2.2, sec.5.3.3) --------------------
+__constant__ uint32_t kK256[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+__constant__ uint32_t kIV256[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) {
+  return __builtin_amdgcn_perm(x, x, 0x00010203u);
+}
+
+// A block as 32 big-endian-assembled dwords (SHA-512: 16 words = 32 dwords,
+// SHA-256: 16 words = 16 dwords; the first BLK/4 entries are used).
+struct Sha512 {
+  static constexpr int BLK = 128;
+  static constexpr int LENB = 16;  // length field bytes
+  uint64_t H[8];
+  __device__ void init() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) H[i] = kIV512_256[i];
+  }
+  // d[] holds the block's 32 dwords in big-endian order (d[2i] = high half)
+  __device__ void compress(const uint32_t (&d)[32]) {
+    uint64_t W[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) W[i] = ((uint64_t)d[2 * i] << 32) | d[2 * i + 1];
+    uint64_t a = H[0], b = H[1], c = H[2], e = H[4], f = H[5], g = H[6], h = H[7], dd = H[3];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+      uint64_t w;
+      if (t < 16) {
+        w = W[t];
+      } else {
+        const uint64_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
+        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+        w = W[t & 15] + s0 + W[(t + 9) & 15] + s1;
+        W[t & 15] = w;
+      }
+      const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+      const uint64_t ch = (e & f) ^ (~e & g);
+      const uint64_t t1 = h + S1 + ch + kK512[t] + w;
+      const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+      const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
+      const uint64_t t2 = S0 + maj;
+      h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
+    }
+    H[0] += a; H[1] += b; H[2] += c; H[3] += dd; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+  }
+  // SHA-512/256: the first 32 bytes of the big-endian state
+  __device__ void out(uint8_t* dst) const {
+    uint32_t* o = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = bswap32((uint32_t)(H[i] >> 32));
+      o[2 * i + 1] = bswap32((uint32_t)H[i]);
+    }
+  }
+};
+
+struct Sha256 {
+  static constexpr int BLK = 64;
+  static constexpr int LENB = 8;
+  uint32_t H[8];
+  __device__ void init() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) H[i] = kIV256[i];
+  }
+  __device__ void compress(const uint32_t (&d)[32]) {
+    uint32_t W[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) W[i] = d[i];
+    uint32_t a = H[0], b = H[1], c = H[2], dd = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      uint32_t w;
+      if (t < 16) {
+        w = W[t];
+      } else {
+        const uint32_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
+        const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+        const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+        w = W[t & 15] + s0 + W[(t + 9) & 15] + s1;
+        W[t & 15] = w;
+      }
+      const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+      const uint32_t ch = (e & f) ^ (~e & g);
+      const uint32_t t1 = h + S1 + ch + kK256[t] + w;
+      const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+      const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+      const uint32_t t2 = S0 + maj;
+      h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
+    }
+    H[0] += a; H[1] += b; H[2] += c; H[3] += dd; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+  }
+  __device__ void out(uint8_t* dst) const {
+    uint32_t* o = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = bswap32(H[i]);
+  }
+};
+
+// Full block at blob + pos (pos + BLK <= len): aligned dwordx4 loads over the
+// 16-byte-aligned window, re-aligned with v_alignbyte, big-endian assembled.
+template <int BLK>
+__device__ __forceinline__ void load_block(const uint8_t* blob, uint64_t pos, uint64_t len,
+                                           uint32_t (&d)[32]) {
+  constexpr int ND = BLK / 4;
+  const uint64_t a0 = pos & ~15ull;
+  const uint32_t sh = (uint32_t)(pos & 15u);
+  if (a0 + BLK + 16 <= len) {
+    uint32_t raw[ND + 4];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* p = reinterpret_cast<const u32x4*>(blob + a0);
+#pragma unroll
+    for (int i = 0; i < ND / 4 + 1; ++i) {
+      const u32x4 v = __builtin_nontemporal_load(p + i);
+      raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
+    }
+    const uint32_t dsh = sh >> 2, bsh = (sh & 3u) * 8u;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      // dword i of the block = bytes [pos + 4i, pos + 4i + 4): raw[dsh + i], raw[dsh + i + 1]
+      uint32_t lo = raw[i], hi = raw[i + 1];
+      // select by dsh (0..3) without dynamic register indexing
+#pragma unroll
+      for (int s = 1; s < 4; ++s) {
+        lo = dsh == (uint32_t)s ? raw[i + s] : lo;
+        hi = dsh == (uint32_t)s ? raw[i + s + 1] : hi;
+      }
+      const uint32_t v = bsh ? __builtin_amdgcn_alignbit(hi, lo, bsh) : lo;
+      d[i] = bswap32(v);
+    }
+  } else {  // near the blob end: byte loads
+#pragma unroll 4
+    for (int i = 0; i < ND; ++i) {
+      uint32_t v = 0;
+      for (int k = 0; k < 4; ++k) v = (v << 8) | blob[pos + 4 * i + k];
+      d[i] = v;
+    }
+  }
+}
+
+// Padded tail block: r = remaining message bytes (r < BLK, or r == BLK on no
+// path), `marker` = whether the 0x80 byte goes into this block, `lenhere` =
+// whether the bit length goes into this block.
+template <int BLK, int LENB>
+__device__ __forceinline__ void tail_block(const uint8_t* p, uint32_t r, bool marker, bool lenhere,
+                                           uint64_t bits, uint32_t (&d)[32]) {
+  constexpr int ND = BLK / 4;
+  for (int i = 0; i < ND; ++i) {
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t idx = (uint32_t)(4 * i + k);
+      uint32_t byte = 0;
+      if (idx < r) byte = p[idx];
+      else if (idx == r && marker) byte = 0x80u;
+      v = (v << 8) | byte;
+    }
+    d[i] = v;
+  }
+  if (lenhere) {  // big-endian bit length in the last LENB bytes (high part 0)
+    d[ND - 2] = (uint32_t)(bits >> 32);
+    d[ND - 1] = (uint32_t)bits;
+  }
+}
+
+template <class H>
+__global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
+  constexpr int BLK = H::BLK;
+  const uint32_t lane = threadIdx.x & 63u;
+  // chunk state
+  uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // first chunk: static
+  uint64_t s = 0, e = 0, pos = 0;
+  uint32_t phase = 0;  // 0 = data blocks, 1 = tail with marker, 2 = length-only block
+  H st;
+  auto start_chunk = [&]() {
+    if (ci < a.n) {
+      s = ci == 0 ? a.first_start : a.ends[ci - 1];
+      e = a.ends[ci];
+      pos = s;
+      phase = 0;
+      st.init();
+    }
+  };
+  if (ci >= a.nfirst) ci = a.n;  // (grid larger than the static share)
+  start_chunk();
+  while (true) {
+    const bool live = ci < a.n;
+    if (__ballot(live) == 0) break;
+    uint32_t d[32];
+    bool finished = false;
+    if (live) {
+      const uint64_t r = e - pos;
+      if (phase == 0 && r >= (uint64_t)BLK) {
+        load_block<BLK>(a.blob, pos, a.len, d);
+        pos += BLK;
+      } else {
+        const uint64_t bits = (e - s) * 8u;
+        if (phase == 0) {
+          // r < BLK message bytes + 0x80; the length fits if r < BLK - LENB
+          const bool fits = r < (uint64_t)(BLK - H::LENB);
+          tail_block<BLK, H::LENB>(a.blob + pos, (uint32_t)r, true, fits, bits, d);
+          pos = e;
+          phase = fits ? 3 : 2;
+        } else {  // phase 2: zeros + length
+          tail_block<BLK, H::LENB>(a.blob + pos, 0u, false, true, bits, d);
+          phase = 3;
+        }
+      }
+    }
+    st.compress(d);  // (dead lanes compress garbage; their state is discarded)
+    if (live && phase == 3) {
+      st.out(a.ids + ci * 32u);
+      finished = true;
+    }
+    // refill the finished lanes from the queue (one atomic per wave)
+    const uint64_t fm = __ballot(finished);
+    if (fm) {
+      const uint32_t nf = (uint32_t)__popcll(fm);
+      uint32_t base = 0;
+      if (lane == (uint32_t)(__ffsll((long long)fm) - 1)) base = atomicAdd(a.queue, nf);
+      base = __shfl(base, __ffsll((long long)fm) - 1, 64);
+      if (finished) {
+        const uint32_t rank = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+        ci = (uint64_t)a.nfirst + base + rank;
+        start_chunk();
+      }
+    }
+  }
+}
+
+template __global__ void digest_kernel<Sha512>(DigestArgs);
+template __global__ void digest_kernel<Sha256>(DigestArgs);
+
+}  // namespace dsx

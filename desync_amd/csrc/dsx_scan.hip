@@ -57,6 +57,23 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t
       : "memory");
 }
 
+// L2 prefetch: one dword per lane (buffer_load_dword ... lds) into the first
+// 256 B of a staging slot that the next DMA overwrites (loads retire in issue
+// order, so the real data lands last); the line it touches is in L2/MALL when
+// that lane's real DMA reaches it a few batches later.
+__device__ __forceinline__ void prefetch4(const u32x4& rsrc, uint32_t voff, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds_addr), "s"(rsrc)
+      : "memory");
+}
+
 // h % d == d-1 on the GPU.
 //   MODE 0: exactly Go's multiply-inverse form (chunker.go:265): v_mul_lo_u32.
 //   MODE 1: one fma lands h/d - (d-1)/d in [2^23, 2^24) where float spacing
@@ -208,7 +225,7 @@ __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t
 // wave, W waves per workgroup (one workgroup per CU: the 64 KiB table is
 // per workgroup).  With NBUF == 1 the row is copied to registers before the
 // refill is issued, so LDS + registers still double-buffer.
-template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB>
+template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   constexpr int BB = BR * kRound;        // batch bytes per lane
   constexpr int NC = BB / 16;            // 16 B chunks per lane row
@@ -361,11 +378,13 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
     // first batch so the steady-state loop has no branch around the rounds
     // (a branch lets the compiler hoist all of a round's table addresses)
     auto batch = [&](uint32_t b, auto first) {
-      // batch b has landed once at most NBUF-1 younger batches are pending
+      // batch b has landed once at most NBUF-1 younger batches (and the one
+      // prefetch issued after b's DMA) are pending
+      static_assert(!PF || NBUF > 1, "prefetch needs double buffering");
       if constexpr (NBUF == 1) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (NBUF - 1)) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (NBUF - 1) + (PF ? 1 : 0)) : "memory");
       }
       const uint32_t slot = NBUF == 1 ? 0u : gb % NBUF;
       const uint8_t* my_row = stage + slot * STG + lane * (uint32_t)BB;
@@ -381,6 +400,11 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
         w[4 * c + 3] = q.w;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (PF && VARIANT != 4) {  // always one op per batch (vmcnt counting)
+        const uint32_t pb = b + NBUF + a.pf_batches;
+        const uint32_t vo = pb < NB ? lane * S + pb * (uint32_t)BB + hfix : 0xFFFFFFF0u;
+        prefetch4(rsrc, vo, stage_lds + slot * (uint32_t)STG);
+      }
       // refill the slot just copied (lands during hashing): this region's
       // batch b+NBUF, or the next region's first batches
       if (b + NBUF < NB)
@@ -455,16 +479,17 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the trailing zero loads
 }
 
-#define DSX_SCAN_INST(BR, NBUF, W, SUB)                                   \
-  template __global__ void scan_kernel<0, 0, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<1, 0, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<2, 0, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<2, 1, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<2, 3, BR, NBUF, W, SUB>(ScanArgs); \
-  template __global__ void scan_kernel<2, 4, BR, NBUF, W, SUB>(ScanArgs);
-DSX_SCAN_INST(2, 2, 8, 8)
-DSX_SCAN_INST(1, 2, 12, 4)
-DSX_SCAN_INST(1, 2, 16, 4)
+#define DSX_SCAN_INST(BR, NBUF, W, SUB, PF)                                   \
+  template __global__ void scan_kernel<0, 0, BR, NBUF, W, SUB, PF>(ScanArgs); \
+  template __global__ void scan_kernel<1, 0, BR, NBUF, W, SUB, PF>(ScanArgs); \
+  template __global__ void scan_kernel<2, 0, BR, NBUF, W, SUB, PF>(ScanArgs); \
+  template __global__ void scan_kernel<2, 1, BR, NBUF, W, SUB, PF>(ScanArgs); \
+  template __global__ void scan_kernel<2, 3, BR, NBUF, W, SUB, PF>(ScanArgs); \
+  template __global__ void scan_kernel<2, 4, BR, NBUF, W, SUB, PF>(ScanArgs);
+DSX_SCAN_INST(2, 2, 8, 8, false)
+DSX_SCAN_INST(2, 2, 8, 8, true)
+DSX_SCAN_INST(1, 2, 12, 4, false)
+DSX_SCAN_INST(1, 2, 16, 4, false)
 
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1
 // (the plain form of chunker_test.go:190-213).  Diagnostic entry point.

@@ -7,17 +7,14 @@ Reference interface (make.go):
     type ChunkingStats struct{ ChunksAccepted, ChunksProduced uint64 }   :330-333
 
 The reference fans the Chunker out over n goroutines (split-and-align); here
-the whole cut list comes from the GPU (dsx_cut_fd: pinned H2D pipeline ->
-scan -> stitch), so ``n`` only caps the host threads hashing chunk IDs.
-Chunk IDs (Digest.Sum, make.go:223) are computed on the host with the
-reference's algorithm (SHA-512/256 by default) -- the GPU digest is the next
-step.
+the file is read into HBM once and both the cut list (scan -> stitch) and
+the chunk IDs (Digest.Sum, make.go:223: SHA-512/256 by default, SHA-256
+alternative) are computed on the GPU.
 """
 from __future__ import annotations
 
 import ctypes
 import os
-from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 
 import numpy as np
@@ -117,32 +114,75 @@ def cut_device_result(ctx=None):
     return n.value
 
 
+def chunk_ids(ptr, length, ends, start=0, ctx=None, algo=None):
+    """Digest.Sum of every chunk of a device-resident blob on the GPU
+    (dsx_chunk_ids; digest.go:11-29, make.go:223).  ``ends`` is a host array of
+    chunk end offsets, the first chunk starts at ``start``.  Returns a list of
+    32-byte IDs.  ``algo`` defaults to the package-global Digest."""
+    ctx = ctx or _lib.default_context()
+    if algo is None:
+        algo = (_lib.DSX_DIGEST_SHA512_256 if digest.Digest.Algorithm() == "sha512-256"
+                else _lib.DSX_DIGEST_SHA256)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    out = np.empty((ends.size, 32), dtype=np.uint8)
+    if ends.size:
+        check(lib().dsx_chunk_ids(ctx.h, ctypes.c_void_p(ptr), length, start, ends.ctypes.data,
+                                  ends.size, out.ctypes.data, 0, algo), ctx.h)
+    return [bytes(r) for r in out]
+
+
+def _file_to_device(f, size, device):
+    """The whole file in HBM (288 GB per MI355X), read in 256 MiB pieces."""
+    import torch
+    t = torch.empty(max(size, 1), dtype=torch.uint8, device=f"cuda:{device}")
+    piece = 256 << 20
+    host = torch.empty(min(piece, max(size, 1)), dtype=torch.uint8).pin_memory()
+    off = 0
+    while off < size:
+        n = min(piece, size - off)
+        got = f.readinto(memoryview(host.numpy())[:n])
+        if got != n:
+            raise OSError(f"short read at offset {off}")
+        t[off:off + n].copy_(host[:n])
+        off += n
+    torch.cuda.synchronize(device)
+    return t
+
+
 def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0):
     """make.go:22-163 -- chunk a file into an Index (not stored anywhere).
 
-    ``ctx`` mirrors the Go context: any object with a ``done()`` method (or
-    None); when it reports done, Interrupted is raised (make.go:201-203).
+    The file is read into HBM once; the cut list (dsx_cut_device) and the
+    chunk IDs (dsx_chunk_ids) are computed there.  ``n`` (the reference's
+    worker count) has no effect on the result, as in the reference.  ``ctx``
+    mirrors the Go context: any object with a ``done()`` method (or None);
+    when it reports done, Interrupted is raised (make.go:201-203).
     """
     pb = pb or NullProgressBar()
     stats = ChunkingStats()
     flags = CaFormatExcludeNoDump
     if digest.Digest.Algorithm() == "sha512-256":
         flags |= CaFormatSHA512256  # make.go:35-38
-    params = Params(min_size, avg_size, max_size)  # NewChunker validation, make.go:103
+    Params(min_size, avg_size, max_size)  # NewChunker validation, make.go:103
     index = Index(FormatIndex(flags, min_size, avg_size, max_size), [])
     with open(name, "rb") as f:
         head = f.read(64)
         index.Index.FeatureFlags |= catar_feature_flags(head)  # make.go:49-61
         size = os.fstat(f.fileno()).st_size  # GetFileSize, make.go:64
+        f.seek(0)
         pb.SetTotal(size)
         pb.Start()
         try:
             if ctx is not None and getattr(ctx, "done", lambda: False)():
                 raise Interrupted()
             dctx = _lib.default_context(device)
-            ends = cut_fd(f.fileno(), min_size, avg_size, max_size, 0, size, ctx=dctx)
+            blob = _file_to_device(f, size, device)
+            ends = cut_device(blob.data_ptr(), size, min_size, avg_size, max_size, ctx=dctx)
+            if ctx is not None and getattr(ctx, "done", lambda: False)():
+                raise Interrupted()
+            ids = chunk_ids(blob.data_ptr(), size, ends, 0, ctx=dctx)
+            del blob
             starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64) if ends.size else ends
-            ids = _chunk_ids(f.fileno(), starts, ends, max(1, int(n)))
             for s, e, cid in zip(starts.tolist(), ends.tolist(), ids):
                 index.Chunks.append(IndexChunk(ID=cid, Start=s, Size=e - s))
                 pb.Set(e)
@@ -150,18 +190,4 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
             stats.ChunksProduced = len(index.Chunks)
         finally:
             pb.Finish()
-    del params
     return index, stats
-
-
-def _chunk_ids(fd, starts, ends, n):
-    """Digest.Sum per chunk (make.go:223); n host threads."""
-    def one(i):
-        s, e = int(starts[i]), int(ends[i])
-        return digest.Digest.Sum(os.pread(fd, e - s, s))
-
-    idx = range(len(starts))
-    if n <= 1 or len(starts) < 2:
-        return [one(i) for i in idx]
-    with ThreadPoolExecutor(max_workers=n) as ex:
-        return list(ex.map(one, idx))

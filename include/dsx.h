@@ -186,6 +186,17 @@ int dsx_gen_uniform(dsx_ctx_t *ctx, void *d_dst, uint64_t offset, uint64_t len, 
 int dsx_gen_dedup(dsx_ctx_t *ctx, void *d_dst, uint64_t offset, uint64_t len, uint64_t seed,
                   double p_repeat);
 
+/* ---- chunk IDs on the GPU (Digest.Sum per chunk: digest.go:11-29, make.go:223,
+ * nullchunk.go:17-23) ------------------------------------------------------- */
+#define DSX_DIGEST_SHA512_256 0 /* desync's default Digest (digest.go:22) */
+#define DSX_DIGEST_SHA256 1     /* the --digest sha256 alternative (digest.go:28) */
+#define DSX_ENDS_DEVICE 4u      /* flag: ends[] is device memory (default: host) */
+/* 32-byte IDs of the chunks [start, ends[0]), [ends[0], ends[1]), ... of the
+ * device-resident blob d_blob[0..len): ids receives n*32 bytes, host memory
+ * by default or device memory with DSX_OUT_DEVICE.  Synchronous. */
+int dsx_chunk_ids(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, uint64_t start,
+                  const uint64_t *ends, uint64_t n, void *ids, uint32_t flags, int algo);
+
 /* ---- statistics (ChunkingStats, make.go:329-341 + scan/stitch timings) ------ */
 typedef struct dsx_stats {
     uint64_t chunks;            /* ChunksAccepted */

@@ -242,3 +242,60 @@ def test_config4_zeros(dctx):
     got = desync_amd.cut_device(t.data_ptr(), n, MIN, AVG, MAX, ctx=dctx)
     assert got.size == n // MAX
     assert np.array_equal(got, np.arange(1, n // MAX + 1, dtype=np.uint64) * MAX)
+    # null chunk IDs on the GPU (nullchunk.go:17-23)
+    ids = desync_amd.chunk_ids(t.data_ptr(), n, got[:64], 0, ctx=dctx)
+    null_id = bytes.fromhex("1c8109946feed9f9e9fe4b5144d90f05a50fb3275e848cb72f4b9546d8c533f2")
+    assert all(i == null_id for i in ids)
+
+
+# ---------------------------------------------------------------- chunk IDs
+def _tricky_ends(total, rng):
+    """Chunk ends exercising every SHA-2 padding case: lengths around the
+    block (64/128) and length-field (55/56, 111/112) boundaries, odd starts."""
+    lens = [1, 2, 3, 15, 16, 17, 55, 56, 57, 63, 64, 65, 111, 112, 113, 119, 120, 127, 128, 129,
+            191, 192, 255, 256, 257, 1000, 4096, 65535, 65536, 65537, 262144]
+    lens += [int(x) for x in rng.integers(1, 300_000, size=200)]
+    ends, e = [], 0
+    for ln in lens:
+        if e + ln > total:
+            break
+        e += ln
+        ends.append(e)
+    if ends[-1] != total:
+        ends.append(total)
+    return np.array(ends, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
+def test_chunk_ids_match_hashlib(dctx, algo):
+    """dsx_chunk_ids == Digest.Sum (digest.go:11-29) chunk by chunk."""
+    import hashlib
+    import desync_amd
+    from desync_amd import _lib
+    rng = np.random.default_rng(7)
+    total = (31 << 20) + 13  # odd length: the last chunk ends off any alignment
+    arr = rng.integers(0, 256, size=total, dtype=np.uint8)
+    t = torch_dev(arr)
+    ends = _tricky_ends(total, rng)
+    code = _lib.DSX_DIGEST_SHA512_256 if algo == "sha512-256" else _lib.DSX_DIGEST_SHA256
+    got = desync_amd.chunk_ids(t.data_ptr(), total, ends, 0, ctx=dctx, algo=code)
+    starts = np.concatenate([[0], ends[:-1]])
+    buf = arr.tobytes()
+    for i, (s, e) in enumerate(zip(starts.tolist(), ends.tolist())):
+        want = hashlib.new("sha512_256" if algo == "sha512-256" else "sha256", buf[s:e]).digest()
+        assert got[i] == want, (i, s, e)
+
+
+def test_chunk_ids_default_chunking(dctx):
+    """IDs of the real chunking of a 64 MiB seeded blob (config-2 shape)."""
+    import hashlib
+    import desync_amd
+    arr = o.synth_uniform(5, 0, 64 << 20)
+    t = torch_dev(arr)
+    ends = desync_amd.cut_device(t.data_ptr(), arr.size, MIN, AVG, MAX, ctx=dctx)
+    got = desync_amd.chunk_ids(t.data_ptr(), arr.size, ends, 0, ctx=dctx)
+    starts = np.concatenate([[0], ends[:-1]])
+    buf = arr.tobytes()
+    want = [hashlib.new("sha512_256", buf[s:e]).digest()
+            for s, e in zip(starts.tolist(), ends.tolist())]
+    assert got == want
