@@ -21,7 +21,7 @@ MIN, AVG, MAX = 16 * 1024, 64 * 1024, 256 * 1024
 
 def torch_dev(arr):
     import torch
-    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.uint8)).to("cuda")
+    t = torch.from_numpy(np.array(arr, dtype=np.uint8, copy=True)).to("cuda")
     torch.cuda.synchronize()
     return t
 
@@ -279,7 +279,7 @@ def test_chunk_ids_match_hashlib(dctx, algo):
     ends = _tricky_ends(total, rng)
     code = _lib.DSX_DIGEST_SHA512_256 if algo == "sha512-256" else _lib.DSX_DIGEST_SHA256
     got = desync_amd.chunk_ids(t.data_ptr(), total, ends, 0, ctx=dctx, algo=code)
-    starts = np.concatenate([[0], ends[:-1]])
+    starts = np.concatenate([np.zeros(1, np.uint64), ends[:-1]])
     buf = arr.tobytes()
     for i, (s, e) in enumerate(zip(starts.tolist(), ends.tolist())):
         want = hashlib.new("sha512_256" if algo == "sha512-256" else "sha256", buf[s:e]).digest()
@@ -294,7 +294,7 @@ def test_chunk_ids_default_chunking(dctx):
     t = torch_dev(arr)
     ends = desync_amd.cut_device(t.data_ptr(), arr.size, MIN, AVG, MAX, ctx=dctx)
     got = desync_amd.chunk_ids(t.data_ptr(), arr.size, ends, 0, ctx=dctx)
-    starts = np.concatenate([[0], ends[:-1]])
+    starts = np.concatenate([np.zeros(1, np.uint64), ends[:-1]])
     buf = arr.tobytes()
     want = [hashlib.new("sha512_256", buf[s:e]).digest()
             for s, e in zip(starts.tolist(), ends.tolist())]
