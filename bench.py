@@ -9,7 +9,8 @@ produces the complete cut list in HBM (scan + stitch, libdsx.so).
 N > 1 (one process per GPU, torch.distributed over RCCL): rank r holds bytes
 [r GiB, (r+1) GiB) of an N GiB blob (+64 B halo, regenerated locally), chunks
 it speculatively (dsx_shard_local), all-gathers the small seam records
-(RCCL), and resolves its final cut list (dsx_shard_resolve) -- weak scaling.
+(RCCL, in place in HBM), and resolves its final cut list in HBM
+(dsx_shard_resolve) -- weak scaling.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -42,6 +43,9 @@ def parse():
     ap.add_argument("--workload", default="uniform", choices=["uniform", "dedup", "zeros"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--check", action="store_true",
+                    help="N>1: compare the concatenated per-rank cut lists with one "
+                         "dsx_cut_device over the whole blob on rank 0 (small sizes)")
     return ap.parse_args()
 
 
@@ -115,12 +119,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
+    # one GPU per rank; DSX_DIST_BACKEND=gloo with more ranks than GPUs is a
+    # functional rehearsal of the N>1 path on a one-GPU box (not a measurement)
+    backend = os.environ.get("DSX_DIST_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    ctx = _lib.Context(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    ctx = _lib.Context(gpu)
     n = int(args.gib * GiB)
     p = desync_amd.Params(MIN, AVG, MAX)
     L = _lib.lib()
@@ -132,9 +143,10 @@ def main():
     d_ptr = blob.data_ptr() + halo
     cap = n // MIN + 4
     out = torch.empty(cap, dtype=torch.int64, device="cuda")
-    seam = _lib.Seam()
-    seam_sz = ctypes.sizeof(_lib.Seam)
-    host_out = np.empty(cap, dtype=np.uint64)
+    shard = None
+    if world > 1:
+        from desync_amd.shard import DeviceShard
+        shard = DeviceShard(ctx, d_ptr, halo, rank * n, n, n * world, p)
 
     def step():
         if world == 1:
@@ -144,18 +156,9 @@ def main():
                        ctx.h)
             _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
             return cnt.value
-        total = n * world
-        _lib.check(L.dsx_shard_local(ctx.h, ctypes.c_void_p(d_ptr), halo, rank * n, n, total,
-                                     ctypes.byref(p.c), ctypes.byref(seam)), ctx.h)
-        mine = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(seam), seam_sz)),
-                                dtype=torch.uint8).to("cuda")
-        gathered = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(gathered, mine)
-        allb = b"".join(g.cpu().numpy().tobytes() for g in gathered)
-        arr = (_lib.Seam * world).from_buffer_copy(allb)
-        _lib.check(L.dsx_shard_resolve(ctx.h, arr, world, rank, host_out.ctypes.data, cap,
-                                       ctypes.byref(cnt), 0), ctx.h)
-        return cnt.value
+        # N > 1: chunk this rank's shard, RCCL all-gather of the 16 KiB seam
+        # records in HBM, resolve the seams (desync_amd/shard.py)
+        return shard.run()
 
     cnt = ctypes.c_uint64()
     for _ in range(args.warmup):
@@ -178,12 +181,27 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tdev = "cuda" if backend == "nccl" else "cpu"
+        tt = torch.tensor([dt], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+        tc = torch.tensor([chunks], dtype=torch.int64, device=tdev)
+        dist.all_reduce(tc)
+        chunks = int(tc.item())
     ms_per_step = dt / args.steps * 1000.0
     value = (n * world * args.steps) / dt / GiB
 
+    if args.check and world > 1:
+        mine = torch.from_numpy(shard.cuts().astype(np.int64))
+        lists = [None] * world
+        dist.all_gather_object(lists, mine.tolist())
+        if rank == 0:
+            whole = torch.empty(n * world, dtype=torch.uint8, device="cuda")
+            make_blob(ctx, whole, 0, n * world, args.workload)
+            ref = desync_amd.cut_device(whole.data_ptr(), n * world, MIN, AVG, MAX, ctx=ctx)
+            got = np.array(sum(lists, []), dtype=np.uint64)
+            assert np.array_equal(got, ref), "sharded cut list differs from the single-GPU one"
+            print(f"check ok: {got.size} cuts across {world} shards", file=sys.stderr)
     if rank == 0:
         res = {
             "metric": METRIC,

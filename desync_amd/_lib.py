@@ -35,6 +35,10 @@ DSX_E_INTERRUPTED = -10
 DSX_E_IO = -11
 DSX_E_STATE = -12
 DSX_E_INTERNAL = -13
+DSX_E_RESYNC = -14
+DSX_SEAM_DEVICE = 8
+DSX_SEAM_LAST = 1
+DSX_SEAM_REWALKED = 2
 
 # every symbol include/dsx.h declares (tests check the library exports them)
 EXPORTS = (
@@ -73,7 +77,8 @@ class Seam(ctypes.Structure):
     _fields_ = [
         ("shard_start", ctypes.c_uint64), ("shard_len", ctypes.c_uint64), ("total", ctypes.c_uint64),
         ("first_cand_beyond", ctypes.c_uint64), ("exit_cut", ctypes.c_uint64),
-        ("window_end", ctypes.c_uint64), ("ncands", ctypes.c_uint32), ("ncuts", ctypes.c_uint32),
+        ("window_end", ctypes.c_uint64), ("entry", ctypes.c_uint64),
+        ("ncands", ctypes.c_uint32), ("ncuts", ctypes.c_uint32),
         ("flags", ctypes.c_uint32), ("pad", ctypes.c_uint32),
         ("cands", ctypes.c_uint64 * DSX_SEAM_MAX_CANDS),
         ("cuts", ctypes.c_uint64 * DSX_SEAM_MAX_CUTS),
@@ -132,8 +137,8 @@ def lib():
             "dsx_stream_advance": (i32, [vp, u64]),
             "dsx_stream_done": (i32, [vp]),
             "dsx_stream_chunk_data": (vp, [vp]),
-            "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), P(Seam)]),
-            "dsx_shard_resolve": (i32, [vp, P(Seam), i32, i32, vp, u64, P(u64), u32]),
+            "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), vp, u32]),
+            "dsx_shard_resolve": (i32, [vp, vp, i32, i32, vp, vp, u64, P(u64), u32]),
             "dsx_selftest_boundary": (i32, [vp, P(Params), i32, u64, u64, P(u64)]),
             "dsx_gen_uniform": (i32, [vp, vp, u64, u64, u64]),
             "dsx_gen_dedup": (i32, [vp, vp, u64, u64, u64, ctypes.c_double]),

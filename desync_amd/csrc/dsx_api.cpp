@@ -38,11 +38,22 @@ __global__ void gen_dedup_kernel(uint8_t* dst, uint64_t offset, uint64_t len, ui
                                  uint32_t p_thresh);
 __global__ void boundary_selftest_kernel(TestConsts tc, int mode, uint64_t h0, uint64_t n,
                                          unsigned long long* mismatches);
+__global__ void seam_cands_kernel(PieceCands pc, uint64_t lo, uint64_t wend, dsx_seam_t* seam);
+__global__ void seam_finalize_kernel(dsx_seam_t* seam, const uint64_t* cuts, const DevState* st,
+                                     uint64_t shard_start, uint64_t shard_len, uint64_t total,
+                                     uint64_t wend0, uint64_t entry, uint32_t flags);
 __global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
-                                    uint64_t max, uint64_t* out, uint64_t* info);
+                                    uint64_t max, uint64_t* ext, uint64_t* info);
+__global__ void shard_emit_kernel(const uint64_t* info, const uint64_t* ext, const uint64_t* spec,
+                                  uint64_t nspec, uint64_t* out, uint64_t cap, volatile uint64_t* res);
 }  // namespace dsx
 
 using namespace dsx;
+
+// the seam record is exchanged as raw bytes between ranks (and mirrored by
+// desync_amd/_lib.py::Seam): its layout is part of the ABI
+static_assert(sizeof(dsx_seam_t) == 7 * 8 + 4 * 4 + 8 * (DSX_SEAM_MAX_CANDS + DSX_SEAM_MAX_CUTS),
+              "dsx_seam_t layout");
 
 // --------------------------------------------------------------------------
 // small utilities
@@ -92,7 +103,7 @@ struct dsx_ctx {
   uint32_t lane_bytes_override = 0;  // DSX_LANE_BYTES (tuning; multiple of 48)
   int prefetch_batches = 0;           // DSX_PREFETCH: L2 prefetch distance in DMA batches (0 = off)
   int regions_per_slot = 1;           // DSX_REGIONS_PER_SLOT: scan work units per wave slot
-  int scan_cfg = 0;                   // DSX_SCAN_CFG: 0 = 8 waves x 2 LDS buffers, 1 = 12 x 1, 2 = 16 x 1
+  int scan_cfg = 0;                   // DSX_SCAN_CFG: index into kCfg* (waves, rounds/batch, LDS buffers)
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
   DevBuf<uint32_t> lane_slot;
@@ -108,6 +119,8 @@ struct dsx_ctx {
   HostState* h_state = nullptr;  // pinned mirror published by fixup_kernel
   uint64_t piece_seq = 0;        // global piece counter (overflow parity, freshness)
   bool init_pending = false;     // next scan initialises DevState with init_carry
+  uint64_t last_region_bytes = 0;  // geometry of the last enqueued piece's region lists
+  uint32_t last_nregions = 0, last_region_cap = 0;
   uint64_t init_carry = 0;
 
   // streaming state (Chunker.Next over an io.Reader)
@@ -120,9 +133,17 @@ struct dsx_ctx {
     const uint8_t* last_chunk = nullptr;
   } st;
 
-  // multi-GPU shard state
-  uint64_t shard_start = 0, shard_len = 0, shard_min = 0, shard_max = 0;
-  std::vector<uint64_t> shard_cuts;
+  // multi-GPU shard state (dsx_shard_local -> dsx_shard_resolve)
+  struct Shard {
+    const uint8_t* d = nullptr;  // caller's shard bytes (valid until resolve returns OK)
+    uint64_t halo = 0, start = 0, len = 0, total = 0;
+    dsx_params_t p{};
+    uint64_t nspec = 0;  // speculative cuts in ctx->out
+    bool valid = false;
+  } sh;
+  DevBuf<dsx_seam_t> d_seam, d_all;
+  DevBuf<uint64_t> d_ext, d_info, d_emit;
+  uint64_t* h_res = nullptr;  // pinned: shard_emit_kernel status / count / entry
 
   dsx_stats_t stats{};
   // per-piece timing events of the current call: {before scan, after scan, after gather}
@@ -223,6 +244,7 @@ extern "C" const char* dsx_strerror(int code) {
     case DSX_E_IO: return "I/O error";
     case DSX_E_STATE: return "invalid stream state";
     case DSX_E_INTERNAL: return "internal error";
+    case DSX_E_RESYNC: return "seam records changed: all-gather them again and resolve again";
     default: return "unknown error";
   }
 }
@@ -293,7 +315,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SCAN_VARIANT")) c->variant = atoi(v);
   if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
-  if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(2, std::max(0, atoi(v)));
+  if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
     const long lb = atol(v);
     if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
@@ -308,6 +330,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     CREATE_STEP(hipEventCreateWithFlags(&c->comp_done[i], hipEventDisableTiming));
   }
   CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
+  CREATE_STEP(hipHostMalloc((void**)&c->h_res, 4 * sizeof(uint64_t)));
   memset(c->h_state, 0, sizeof(HostState));
   CREATE_STEP(c->state.ensure(1));
   CREATE_STEP(c->overflow.ensure(4));  // [0..1] overflow, [2..3] scan work queue (parity)
@@ -327,6 +350,8 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
   c->dg_ends.release(); c->dg_ids.release(); c->dg_queue.release();
   c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
+  c->d_seam.release(); c->d_all.release(); c->d_ext.release(); c->d_info.release(); c->d_emit.release();
+  if (c->h_res) (void)hipHostFree(c->h_res);
   c->dbuf[0].release(); c->dbuf[1].release();
   for (auto& p : c->pinned) if (p) (void)hipHostFree(p);
   if (c->h_state) (void)hipHostFree(c->h_state);
@@ -397,8 +422,8 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   // lane segment S = 48*(4k-1): the warm-up round plus S/48 rounds fill k
   // whole 4-round DMA batches
   // scan configs: {waves per workgroup, rounds per DMA batch}
-  static const int kCfgWaves[3] = {8, 12, 16};
-  static const int kCfgBR[3] = {2, 1, 1};
+  static const int kCfgWaves[6] = {8, 12, 16, 12, 8, 16};
+  static const int kCfgBR[6] = {2, 1, 1, 2, 2, 2};
   const int W = kCfgWaves[c->scan_cfg];
   const int cfgBR = kCfgBR[c->scan_cfg];
   const uint64_t slots_total = (uint64_t)c->ncu * W;  // wave slots
@@ -435,6 +460,9 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     rcap = (uint32_t)std::min<double>(64.0 * S, 4.0 * expct + 64.0);
     rcap = (rcap + 63u) & ~63u;
   }
+  c->last_region_bytes = region_bytes;
+  c->last_nregions = (uint32_t)nregions;
+  c->last_region_cap = rcap;
   HIPCHK(c, grow(c, c->lane_slot, nlanes * LS));
   HIPCHK(c, grow(c, c->region_cnt, nregions));
   HIPCHK(c, grow(c, c->region_list, nregions * rcap));
@@ -490,14 +518,16 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     else                                                                                   \
       hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
   } while (0)
-    if (W == 8 && c->prefetch_batches > 0)
-      DSX_LAUNCH(2, 2, 8, 8, true);
-    else if (W == 8)
-      DSX_LAUNCH(2, 2, 8, 8, false);
-    else if (W == 12)
-      DSX_LAUNCH(1, 2, 12, 4, false);
-    else
-      DSX_LAUNCH(1, 2, 16, 4, false);
+    switch (c->scan_cfg) {
+      case 1: DSX_LAUNCH(1, 2, 12, 4, false); break;
+      case 2: DSX_LAUNCH(1, 2, 16, 4, false); break;
+      case 3: DSX_LAUNCH(2, 1, 12, 8, false); break;
+      case 4: DSX_LAUNCH(2, 1, 8, 8, false); break;
+      case 5: DSX_LAUNCH(2, 1, 16, 4, false); break;
+      default:
+        if (c->prefetch_batches > 0) DSX_LAUNCH(2, 2, 8, 8, true);
+        else DSX_LAUNCH(2, 2, 8, 8, false);
+    }
 #undef DSX_LAUNCH
     HIPCHK(c, hipGetLastError());
   }
@@ -1077,43 +1107,50 @@ extern "C" int dsx_selftest_boundary(dsx_ctx_t* c, const dsx_params_t* p, int mo
 // --------------------------------------------------------------------------
 // multi-GPU shards (split-and-align across ranks, make.go:22-163 / 277-327)
 // --------------------------------------------------------------------------
-extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
-                               uint64_t shard_start, uint64_t shard_len, uint64_t total,
-                               const dsx_params_t* p, dsx_seam_t* seam) {
-  if (!c || !p || !seam || (shard_len && !d_shard) || shard_start + shard_len > total)
-    return DSX_E_INVAL;
-  if (shard_start > 0 && halo < kRound) return DSX_E_INVAL;
-  c->cancel.store(0);
-  int rc = ensure_attr_walk(c);
-  if (rc) return rc;
-  memset(seam, 0, sizeof *seam);
-  seam->shard_start = shard_start;
-  seam->shard_len = shard_len;
-  seam->total = total;
-  seam->first_cand_beyond = UINT64_MAX;
-  c->shard_start = shard_start;
-  c->shard_len = shard_len;
-  c->shard_min = p->min;
-  c->shard_max = p->max;
-  const bool is_last = shard_start + shard_len == total;
-  const uint64_t need = shard_len / p->min + 4;
+// Chunks the shard from the cut `entry` (shard_start: speculative, make.go's
+// worker at span*i; or the true entry cut on a re-walk), builds the seam
+// record in c->d_seam, leaves the shard's cuts in c->out and waits.
+static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags) {
+  auto& sh = c->sh;
+  const dsx_params_t* p = &sh.p;
+  const bool is_last = sh.start + sh.len == sh.total;
+  const uint64_t need = sh.len / p->min + 4;
+  const uint64_t wend0 = sh.start + std::min<uint64_t>(sh.len, 32 * p->max);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, grow(c, c->d_seam, 1));
   for (int attempt = 0; attempt < 2; ++attempt) {
+    if (c->cancel.load()) return DSX_E_INTERRUPTED;
     HIPCHK(c, grow(c, c->out, need));
-    CallCfg cc{p, total, shard_start, kRound, c->out.p, need, attempt == 1};
-    cc.halo0 = shard_start > 0 ? halo : 0;
-    // the speculative chain starts at the virtual cut shard_start; the piece
-    // is final only for the last shard
-    HIPCHK(c, hipSetDevice(c->device));
-    rc = reset_state(c, shard_start);
+    CallCfg cc{p, sh.total, entry, kRound, c->out.p, need, attempt == 1};
+    cc.halo0 = sh.start > 0 ? sh.halo : 0;
+    int rc = reset_state(c, entry);
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
     const uint64_t piece = cc.dense ? kDensePiece : kPieceMax;
-    for (uint64_t off = 0; off < shard_len; off += piece) {
-      const uint64_t n = std::min(piece, shard_len - off);
-      rc = enqueue_piece(c, cc, (const uint8_t*)d_shard + off, off + cc.halo0, shard_start + off,
-                         n, is_last && off + n == shard_len);
+    for (uint64_t off = 0; off < sh.len; off += piece) {
+      const uint64_t n = std::min(piece, sh.len - off);
+      rc = enqueue_piece(c, cc, sh.d + off, off + cc.halo0, sh.start + off, n,
+                         is_last && off + n == sh.len);
       if (rc) return rc;
+      if (off == 0) {
+        // the window candidates come from the first piece's region lists
+        PieceCands pc{};
+        pc.P = sh.start;
+        pc.RB = c->last_region_bytes;
+        pc.nregions = c->last_nregions;
+        pc.region_cap = c->last_region_cap;
+        pc.region_cnt = c->region_cnt.p;
+        pc.region_list = c->region_list.p;
+        pc.overflow = nullptr;
+        hipLaunchKernelGGL(seam_cands_kernel, dim3(1), dim3(64), 0, c->stream, pc, sh.start, wend0,
+                           c->d_seam.p);
+        HIPCHK(c, hipGetLastError());
+      }
     }
+    hipLaunchKernelGGL(seam_finalize_kernel, dim3(1), dim3(1), 0, c->stream, c->d_seam.p,
+                       (const uint64_t*)c->out.p, (const DevState*)c->state.p, sh.start, sh.len,
+                       sh.total, wend0, entry, (is_last ? (uint32_t)DSX_SEAM_LAST : 0u) | rec_flags);
+    HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
     HostState st;
     rc = read_state(c, &st);
@@ -1126,108 +1163,118 @@ extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
       c->err = "shard: stitch error";
       return DSX_E_INTERNAL;
     }
-    c->shard_cuts.resize(st.total);
-    if (st.total)
-      HIPCHK(c, hipMemcpy(c->shard_cuts.data(), c->out.p, st.total * 8, hipMemcpyDeviceToHost));
-    seam->exit_cut = st.carry;
-    // seam window: candidates and spec cuts of the shard's first bytes
-    uint64_t wend = shard_start + std::min<uint64_t>(shard_len, 32 * p->max);
-    // candidates in (shard_start, wend]: they come from the last piece scanned only
-    // when the shard fits one piece; rescan the window as its own piece otherwise
-    std::vector<uint64_t> cands;
-    {
-      const uint64_t wlen = wend - shard_start;
-      CallCfg wc{p, total, shard_start, kRound, c->out.p, need, true};
-      wc.halo0 = cc.halo0;
-      rc = reset_state(c, shard_start);
-      if (rc) return rc;
-      rc = enqueue_piece(c, wc, (const uint8_t*)d_shard, wc.halo0, shard_start, wlen,
-                         is_last && wlen == shard_len);
-      if (rc) return rc;
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      // read back the region lists of the dense-path scan of the window
-      const uint64_t RB = 64ull * kDenseS;
-      const uint64_t nr = (wlen + RB - 1) / RB;
-      const uint64_t cap = RB;  // dense path: region_cap == region bytes
-      std::vector<uint32_t> cnt(nr);
-      std::vector<uint32_t> lst(nr * cap);
-      HIPCHK(c, hipMemcpy(cnt.data(), c->region_cnt.p, nr * 4, hipMemcpyDeviceToHost));
-      HIPCHK(c, hipMemcpy(lst.data(), c->region_list.p, nr * cap * 4, hipMemcpyDeviceToHost));
-      for (uint64_t r = 0; r < nr; ++r)
-        for (uint32_t i = 0; i < cnt[r] && i < cap; ++i)
-          cands.push_back(shard_start + r * RB + lst[r * cap + i]);
-    }
-    if (cands.size() > DSX_SEAM_MAX_CANDS) {
-      seam->first_cand_beyond = cands[DSX_SEAM_MAX_CANDS];
-      wend = cands[DSX_SEAM_MAX_CANDS - 1];
-      cands.resize(DSX_SEAM_MAX_CANDS);
-    }
-    uint32_t nc = 0;
-    for (uint64_t x : c->shard_cuts) {
-      if (x > wend) break;
-      if (nc == DSX_SEAM_MAX_CUTS) {
-        wend = seam->cuts[nc - 1];
-        break;
-      }
-      seam->cuts[nc++] = x;
-    }
-    uint32_t ncand = 0;
-    for (uint64_t x : cands)
-      if (x <= wend) seam->cands[ncand++] = x;
-    seam->ncands = ncand;
-    seam->ncuts = nc;
-    seam->window_end = wend;
-    seam->flags = is_last ? 1u : 0u;
+    sh.nspec = st.total;
+    c->stats.chunks = st.total;
     return DSX_OK;
   }
   c->err = "dense-candidate path overflowed";
   return DSX_E_INTERNAL;
 }
 
-extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks, int rank,
-                                 uint64_t* out_ends, uint64_t cap, uint64_t* n_out,
-                                 uint32_t flags) {
-  if (!c || !all || nranks < 1 || rank < 0 || rank >= nranks || !n_out) return DSX_E_INVAL;
-  (void)flags;
-  HIPCHK(c, hipSetDevice(c->device));
-  const dsx_params_t* pp = nullptr;
-  (void)pp;
-  DevBuf<dsx_seam_t> d_all;
-  DevBuf<uint64_t> d_out, d_info;
-  HIPCHK(c, d_all.ensure(nranks));
-  HIPCHK(c, d_out.ensure(DSX_SEAM_MAX_CUTS + 4));
-  HIPCHK(c, d_info.ensure(8));
-  HIPCHK(c, hipMemcpyAsync(d_all.p, all, sizeof(dsx_seam_t) * nranks, hipMemcpyHostToDevice,
-                           c->stream));
-  hipLaunchKernelGGL(seam_resolve_kernel, dim3(1), dim3(64), 0, c->stream, d_all.p, nranks, rank,
-                     c->shard_min, c->shard_max, d_out.p, d_info.p);
-  HIPCHK(c, hipGetLastError());
-  uint64_t info[8];
-  HIPCHK(c, hipMemcpyAsync(info, d_info.p, sizeof info, hipMemcpyDeviceToHost, c->stream));
+// Copies the ctx's seam record to the caller's (host or device) record.
+static int seam_out(dsx_ctx* c, dsx_seam_t* seam, bool dev) {
+  HIPCHK(c, hipMemcpyAsync(seam, c->d_seam.p, sizeof(dsx_seam_t),
+                           dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  // info: [0]=status (0 ok, else failing seam + 1), [1]=entry cut c_r, [2]=#ext cuts
-  if (info[0] != 0) {
-    char b[160];
-    snprintf(b, sizeof b, "seam %llu did not converge inside its window",
-             (unsigned long long)(info[0] - 1));
-    c->err = b;
-    d_all.release(); d_out.release(); d_info.release();
+  return DSX_OK;
+}
+
+extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
+                               uint64_t shard_start, uint64_t shard_len, uint64_t total,
+                               const dsx_params_t* p, dsx_seam_t* seam, uint32_t flags) {
+  if (!c || !p || !seam || (shard_len && !d_shard) || shard_start + shard_len > total ||
+      (flags & ~DSX_SEAM_DEVICE) != 0)
+    return DSX_E_INVAL;
+  if (shard_start > 0 && halo < kRound) return DSX_E_INVAL;
+  c->cancel.store(0);
+  int rc = ensure_attr_walk(c);
+  if (rc) return rc;
+  auto& sh = c->sh;
+  sh.d = (const uint8_t*)d_shard;
+  sh.halo = halo;
+  sh.start = shard_start;
+  sh.len = shard_len;
+  sh.total = total;
+  sh.p = *p;
+  sh.nspec = 0;
+  sh.valid = false;
+  if (shard_len == 0) {
+    dsx_seam_t z;
+    memset(&z, 0, sizeof z);
+    z.shard_start = z.exit_cut = z.window_end = z.entry = shard_start;
+    z.total = total;
+    z.first_cand_beyond = UINT64_MAX;
+    z.flags = shard_start == total ? DSX_SEAM_LAST : 0u;
+    HIPCHK(c, grow(c, c->d_seam, 1));
+    HIPCHK(c, hipMemcpyAsync(c->d_seam.p, &z, sizeof z, hipMemcpyHostToDevice, c->stream));
+    sh.valid = true;
+    return seam_out(c, seam, (flags & DSX_SEAM_DEVICE) != 0);
+  }
+  rc = shard_run(c, shard_start, 0u);
+  if (rc) return rc;
+  sh.valid = true;
+  return seam_out(c, seam, (flags & DSX_SEAM_DEVICE) != 0);
+}
+
+extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks, int rank,
+                                 dsx_seam_t* my_seam, uint64_t* out_ends, uint64_t cap,
+                                 uint64_t* n_out, uint32_t flags) {
+  if (!c || !all || nranks < 1 || rank < 0 || rank >= nranks || !n_out || !my_seam ||
+      (cap && !out_ends) || (flags & ~(DSX_SEAM_DEVICE | DSX_OUT_DEVICE)) != 0)
+    return DSX_E_INVAL;
+  auto& sh = c->sh;
+  if (!sh.valid) return DSX_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool seam_dev = (flags & DSX_SEAM_DEVICE) != 0, out_dev = (flags & DSX_OUT_DEVICE) != 0;
+  const dsx_seam_t* d_all = all;
+  if (!seam_dev) {
+    HIPCHK(c, grow(c, c->d_all, (size_t)nranks));
+    HIPCHK(c, hipMemcpyAsync(c->d_all.p, all, sizeof(dsx_seam_t) * nranks, hipMemcpyHostToDevice,
+                             c->stream));
+    d_all = c->d_all.p;
+  }
+  HIPCHK(c, grow(c, c->d_ext, DSX_SEAM_MAX_CUTS + 4));
+  HIPCHK(c, grow(c, c->d_info, 8));
+  hipLaunchKernelGGL(seam_resolve_kernel, dim3(1), dim3(64), 0, c->stream, d_all, nranks, rank,
+                     sh.p.min, sh.p.max, c->d_ext.p, c->d_info.p);
+  HIPCHK(c, hipGetLastError());
+  const uint64_t most = sh.nspec + DSX_SEAM_MAX_CUTS;
+  uint64_t* dst = out_ends;
+  uint64_t dcap = cap;
+  if (!out_dev) {
+    HIPCHK(c, grow(c, c->d_emit, most));
+    dst = c->d_emit.p;
+    dcap = most;
+  }
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((most + 255) / 256, 4096);
+  c->h_res[0] = ~0ull;
+  hipLaunchKernelGGL(shard_emit_kernel, dim3(blocks), dim3(256), 0, c->stream,
+                     (const uint64_t*)c->d_info.p, (const uint64_t*)c->d_ext.p,
+                     (const uint64_t*)c->out.p, sh.nspec, dst, dcap, (volatile uint64_t*)c->h_res);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t status = c->h_res[0], n = c->h_res[1], entry = c->h_res[2];
+  if (status == ~0ull) {
+    c->err = "shard: resolve did not publish its result";
     return DSX_E_INTERNAL;
   }
-  std::vector<uint64_t> ext(info[2]);
-  if (info[2]) HIPCHK(c, hipMemcpy(ext.data(), d_out.p, info[2] * 8, hipMemcpyDeviceToHost));
-  d_all.release(); d_out.release(); d_info.release();
-  // this rank's cuts: ext cuts in (start, c_r) followed by spec cuts >= c_r
-  const uint64_t cr = info[1];
-  uint64_t n = 0;
-  std::vector<uint64_t> res;
-  res.reserve(ext.size() + c->shard_cuts.size());
-  for (uint64_t x : ext) res.push_back(x);
-  for (uint64_t x : c->shard_cuts)
-    if (x >= cr) res.push_back(x);
-  n = res.size();
+  if (status != 0) {
+    // seam `status - 1` did not converge inside its window: its owner re-walks
+    // its shard from the true entry cut and republishes its record
+    *n_out = 0;
+    const int failing = (int)(status - 1);
+    if (failing == rank) {
+      int rc = shard_run(c, entry, DSX_SEAM_REWALKED);
+      if (rc) return rc;
+      c->stats.repaired_segments++;
+      rc = seam_out(c, my_seam, seam_dev);
+      if (rc) return rc;
+    }
+    return DSX_E_RESYNC;
+  }
   *n_out = n;
   if (n > cap) return DSX_E_CAPACITY;
-  if (n) memcpy(out_ends, res.data(), n * 8);
+  if (!out_dev && n)
+    HIPCHK(c, hipMemcpy(out_ends, c->d_emit.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return DSX_OK;
 }

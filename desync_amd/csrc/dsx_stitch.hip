@@ -472,6 +472,76 @@ __global__ __launch_bounds__(256) void gather_kernel(StitchArgs a) {
 
 namespace dsx {
 
+// Candidates of a piece in (lo, wend], in order, from the scan's region lists:
+// the first DSX_SEAM_MAX_CANDS go to seam->cands, the next one (if any) to
+// seam->first_cand_beyond.  One wavefront; runs after the piece's scan and
+// before the next piece's scan overwrites the lists.
+__global__ __launch_bounds__(64) void seam_cands_kernel(PieceCands pc, uint64_t lo, uint64_t wend,
+                                                        dsx_seam_t* seam) {
+  const uint32_t lane = threadIdx.x;
+  constexpr uint32_t kMax = DSX_SEAM_MAX_CANDS;
+  uint32_t n = 0;  // wave-uniform
+  const uint64_t r0 = lo > pc.P ? (lo - pc.P) / pc.RB : 0;
+  for (uint64_t r = r0; r < pc.nregions && n <= kMax; ++r) {
+    const uint64_t base = pc.P + r * pc.RB;  // region covers (base, base + RB]
+    if (base >= wend) break;
+    const uint32_t cnt0 = pc.region_cnt[r];
+    const uint32_t cnt = cnt0 < pc.region_cap ? cnt0 : pc.region_cap;
+    const uint32_t* l = pc.region_list + r * (uint64_t)pc.region_cap;
+    for (uint32_t i0 = 0; i0 < cnt && n <= kMax; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const uint64_t p = i < cnt ? base + l[i] : 0;
+      const bool ok = i < cnt && p > lo && p <= wend;
+      const uint64_t m = __ballot(ok);
+      const uint32_t idx = n + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (ok) {
+        if (idx < kMax) seam->cands[idx] = p;
+        else if (idx == kMax) seam->first_cand_beyond = p;
+      }
+      n += (uint32_t)__popcll(m);
+    }
+  }
+  if (lane == 0) {
+    seam->ncands = n < kMax ? n : kMax;
+    if (n <= kMax) seam->first_cand_beyond = ~0ull;
+  }
+}
+
+// Completes a seam record once the shard's chain is known: truncates the
+// window to the candidate and cut capacities (as the CPU restatement
+// oracle/seam.py does), copies the speculative cuts of the window and the
+// exit cut.  One thread.
+__global__ void seam_finalize_kernel(dsx_seam_t* seam, const uint64_t* cuts, const DevState* st,
+                                     uint64_t shard_start, uint64_t shard_len, uint64_t total,
+                                     uint64_t wend0, uint64_t entry, uint32_t flags) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t wend = wend0;
+  if (seam->first_cand_beyond != ~0ull) wend = seam->cands[DSX_SEAM_MAX_CANDS - 1];
+  const uint64_t n = st->total;
+  uint32_t nc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t x = cuts[i];
+    if (x > wend) break;
+    if (nc == DSX_SEAM_MAX_CUTS) {
+      wend = seam->cuts[nc - 1];
+      break;
+    }
+    seam->cuts[nc++] = x;
+  }
+  uint32_t ncand = 0;
+  while (ncand < seam->ncands && seam->cands[ncand] <= wend) ++ncand;
+  seam->shard_start = shard_start;
+  seam->shard_len = shard_len;
+  seam->total = total;
+  seam->exit_cut = st->carry;
+  seam->window_end = wend;
+  seam->entry = entry;
+  seam->ncands = ncand;
+  seam->ncuts = nc;
+  seam->flags = flags;
+  seam->pad = 0;
+}
+
 struct SeamSrc {
   const uint64_t* c;
   uint32_t n;
@@ -483,54 +553,100 @@ struct SeamSrc {
   }
 };
 
-// One lane walks the true chain across the seams in rank order: the chain
+// One lane walks the true chain across ALL seams in rank order: the chain
 // entering rank r (the exit of rank r-1's chain, true by induction) is walked
 // over rank r's seam window until it lands on a cut of rank r's speculative
-// chain (convergence c_r).  info: [0] 0 or 1+failing rank, [1] c_rank,
-// [2] number of cuts written to out (the true cuts of rank `rank` before c_r).
+// chain (convergence c_r).  A re-walked shard (DSX_SEAM_REWALKED) is true from
+// its recorded entry on.  Every rank checks every seam, so all ranks agree on
+// whether another exchange round is needed.
+// info: [0] 0, or 1 + the first rank whose seam did not converge; [1] c_rank
+// (keep the speculative cuts >= c_rank), or on failure the true entry cut of
+// the failing rank; [2] number of cuts written to ext (the true cuts of
+// `rank` before c_rank).
 __global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
-                                    uint64_t max, uint64_t* out, uint64_t* info) {
+                                    uint64_t max, uint64_t* ext, uint64_t* info) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  info[0] = 0;
-  info[1] = all[rank].shard_start;
-  info[2] = 0;
-  if (rank == 0) return;
+  uint64_t mine_c = all[rank].shard_start, mine_n = 0;
   uint64_t entry = all[0].exit_cut;
-  for (int r = 1; r <= rank && r < nranks; ++r) {
+  for (int r = 1; r < nranks; ++r) {
     const dsx_seam_t& s = all[r];
-    ChainParams w;
-    w.min = min;
-    w.max = max;
-    w.L = s.total;
-    w.PE = s.window_end;
-    w.is_last = s.window_end == s.total ? 1u : 0u;
-    w.pad = 0;
-    SeamSrc src{s.cands, s.ncands, 0};
-    uint64_t x = entry, c = kNone;
+    uint64_t c = kNone;
     uint32_t n = 0;
-    if (x == s.shard_start || s.shard_len == 0) {
+    if (s.flags & DSX_SEAM_REWALKED) {
+      if (entry == s.entry) c = 0;  // the whole re-walked chain is true
+    } else if (entry == s.shard_start || s.shard_len == 0) {
       c = s.shard_start;
     } else {
+      ChainParams w;
+      w.min = min;
+      w.max = max;
+      w.L = s.total;
+      w.PE = s.window_end;
+      w.is_last = s.window_end == s.total ? 1u : 0u;
+      w.pad = 0;
+      SeamSrc src{s.cands, s.ncands, 0};
+      uint64_t x = entry;
       while (true) {
         if (w.is_last && x >= w.L) { c = x; break; }
         const uint64_t nx = next_cut(x, src, w);
         if (nx == kUndet) break;
         const uint32_t idx = bsearch_u64(s.cuts, s.ncuts, nx);
         if (idx < s.ncuts && s.cuts[idx] == nx) { c = nx; break; }
-        if (r == rank && n < DSX_SEAM_MAX_CUTS) out[n++] = nx;
+        if (r == rank && n < DSX_SEAM_MAX_CUTS) ext[n++] = nx;
         x = nx;
       }
     }
     if (c == kNone) {
       info[0] = (uint64_t)r + 1;
+      info[1] = entry;
+      info[2] = 0;
       return;
     }
     if (r == rank) {
-      info[1] = c;
-      info[2] = n;
-      return;
+      mine_c = c;
+      mine_n = n;
     }
     entry = s.shard_len == 0 ? entry : s.exit_cut;
+  }
+  info[0] = 0;
+  info[1] = mine_c;
+  info[2] = mine_n;
+}
+
+// This rank's final cut list = ext cuts, then the speculative cuts >= c_rank;
+// the count and status go to pinned host memory (res[0] status, [1] count,
+// [2] entry of the failing rank).
+__global__ __launch_bounds__(256) void shard_emit_kernel(const uint64_t* info, const uint64_t* ext,
+                                                         const uint64_t* spec, uint64_t nspec,
+                                                         uint64_t* out, uint64_t cap,
+                                                         volatile uint64_t* res) {
+  const uint64_t status = info[0];
+  if (status != 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      res[0] = status;
+      res[1] = 0;
+      res[2] = info[1];
+      __threadfence_system();
+    }
+    return;
+  }
+  const uint64_t cr = info[1], next = info[2];
+  uint64_t lo = 0, hi = nspec;  // first spec cut >= cr
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (spec[m] < cr) lo = m + 1; else hi = m;
+  }
+  const uint64_t n = next + (nspec - lo);
+  if (n <= cap) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+      out[i] = i < next ? ext[i] : spec[lo + (i - next)];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    res[0] = 0;
+    res[1] = n;
+    res[2] = 0;
+    __threadfence_system();
   }
 }
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSX_ABI_VERSION 1
+#define DSX_ABI_VERSION 2
 
 /* ---- error codes (negative) ---------------------------------------------- */
 enum {
@@ -55,7 +55,8 @@ enum {
     DSX_E_INTERRUPTED = -10,     /* dsx_cancel() was called: Interrupted{} errors.go:56-58 */
     DSX_E_IO = -11,              /* read() on the file descriptor failed */
     DSX_E_STATE = -12,           /* call not valid in the current stream state */
-    DSX_E_INTERNAL = -13         /* internal consistency check failed */
+    DSX_E_INTERNAL = -13,        /* internal consistency check failed */
+    DSX_E_RESYNC = -14           /* dsx_shard_resolve: exchange the seam records again */
 };
 
 /* ---- chunker parameters ----------------------------------------------------
@@ -144,29 +145,46 @@ const uint8_t *dsx_stream_chunk_data(dsx_ctx_t *ctx);
  * by `halo` readable bytes (halo >= 48, or halo == 0 only when shard_start==0).
  *
  * dsx_shard_local: chunks the shard speculatively from a virtual cut at
- *   shard_start (make.go's worker at span*i, make.go:94-116), keeps the
- *   candidate positions of the first `seam_bytes` of the shard, and fills a
- *   fixed-size seam record (dsx_seam_t) to be all-gathered between ranks.
- * dsx_shard_resolve: given all ranks' seam records (rank order), aligns
- *   every seam (syncWith, make.go:277-298) and returns this rank's final cut
- *   list: the cuts c with shard_start < c <= shard_start+shard_len.
- * Seam records are plain bytes; transport them with RCCL all-gather. */
+ *   shard_start (make.go's worker at span*i, make.go:94-116) and fills a
+ *   fixed-size seam record (dsx_seam_t): the candidates and speculative cuts
+ *   of the shard's first 32*max bytes and the chain's exit cut.  The record is
+ *   built on the device; `seam` is device memory with DSX_SEAM_DEVICE (then it
+ *   can be all-gathered by RCCL in place), host memory otherwise.
+ * dsx_shard_resolve: given all ranks' seam records (rank order, host or
+ *   device memory per DSX_SEAM_DEVICE), walks the true chain across the seams
+ *   (syncWith, make.go:277-298) and writes this rank's final cut list: the
+ *   cuts c with shard_start < c <= shard_start+shard_len (host memory, or
+ *   device memory with DSX_OUT_DEVICE).
+ *   Returns DSX_E_RESYNC when a seam did not converge inside its window (a
+ *   zero run across a shard boundary, README.md:114-119): the rank owning
+ *   that seam has then re-walked its shard from the true entry cut and
+ *   rewritten its record `my_seam` (flag DSX_SEAM_REWALKED); every rank
+ *   all-gathers the records again and calls dsx_shard_resolve again (at most
+ *   nranks rounds).  d_shard passed to dsx_shard_local must stay valid until
+ *   dsx_shard_resolve returns DSX_OK.
+ * Seam records are plain bytes. */
 #define DSX_SEAM_MAX_CANDS 1024
 #define DSX_SEAM_MAX_CUTS 1024
+#define DSX_SEAM_DEVICE 8u      /* flag: seam records are device memory */
+#define DSX_SEAM_LAST 1u        /* seam flags: the shard ends the blob */
+#define DSX_SEAM_REWALKED 2u    /* seam flags: chain re-walked from the true entry `entry` */
 typedef struct dsx_seam {
     uint64_t shard_start, shard_len, total;
     uint64_t first_cand_beyond;   /* first candidate > window end, or UINT64_MAX */
-    uint64_t exit_cut;            /* speculative chain's last cut <= shard end */
+    uint64_t exit_cut;            /* the shard chain's last cut <= shard end */
     uint64_t window_end;          /* candidates/cuts below cover (shard_start, window_end] */
+    uint64_t entry;               /* DSX_SEAM_REWALKED: the entry cut the chain started from */
     uint32_t ncands, ncuts, flags, pad;
     uint64_t cands[DSX_SEAM_MAX_CANDS]; /* candidate positions in (shard_start, window_end] */
     uint64_t cuts[DSX_SEAM_MAX_CUTS];   /* spec chain cuts in (shard_start, window_end] */
 } dsx_seam_t;
 
 int dsx_shard_local(dsx_ctx_t *ctx, const void *d_shard, uint64_t halo, uint64_t shard_start,
-                    uint64_t shard_len, uint64_t total, const dsx_params_t *p, dsx_seam_t *seam);
+                    uint64_t shard_len, uint64_t total, const dsx_params_t *p, dsx_seam_t *seam,
+                    uint32_t flags);
 int dsx_shard_resolve(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, int rank,
-                      uint64_t *out_ends, uint64_t cap, uint64_t *n_out, uint32_t flags);
+                      dsx_seam_t *my_seam, uint64_t *out_ends, uint64_t cap, uint64_t *n_out,
+                      uint32_t flags);
 
 /* ---- diagnostics ------------------------------------------------------------- */
 /* Evaluates the GPU boundary predicate (mode 0: multiply-inverse form of

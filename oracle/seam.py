@@ -47,8 +47,14 @@ def spec_chain(cands, start, mn, mx, L, PE, is_last):
     return cuts
 
 
+SEAM_LAST = 1
+SEAM_REWALKED = 2
+
+
 def shard_local(full, start, length, total, mn, av, mx, max_cands=1024, max_cuts=1024):
-    """Seam record + speculative cut list of one shard (positions absolute)."""
+    """Seam record + speculative cut list + candidates of one shard (absolute
+    positions).  Mirrors dsx_shard_local (seam_cands_kernel /
+    seam_finalize_kernel)."""
     is_last = start + length == total
     lo = max(0, start - 64)
     c = o.candidates(full[lo:start + length], mn, av, mx) + lo  # halo for windows
@@ -70,24 +76,42 @@ def shard_local(full, start, length, total, mn, av, mx, max_cands=1024, max_cuts
     wc = [x for x in wc if x <= wend]
     exit_cut = cuts[-1] if cuts else start
     seam = dict(shard_start=start, shard_len=length, total=total, exit_cut=exit_cut,
-                window_end=wend, cands=wc, cuts=wcuts, flags=1 if is_last else 0)
+                window_end=wend, entry=start, cands=wc, cuts=wcuts,
+                flags=SEAM_LAST if is_last else 0)
+    return seam, cuts, c
+
+
+def rewalk(cands, entry, start, length, total, mn, mx):
+    """The shard's chain re-walked from its true entry cut (dsx_shard_resolve's
+    DSX_E_RESYNC path): every cut of it is true."""
+    is_last = start + length == total
+    cuts = spec_chain(cands, entry, mn, mx, total, start + length, is_last)
+    seam = dict(shard_start=start, shard_len=length, total=total,
+                exit_cut=cuts[-1] if cuts else entry, window_end=start, entry=entry, cands=[],
+                cuts=[], flags=(SEAM_LAST if is_last else 0) | SEAM_REWALKED)
     return seam, cuts
 
 
 def resolve(seams, rank, mn, mx):
-    """(ext cuts, c_rank): the true cuts of `rank` before its convergence point."""
-    if rank == 0:
-        return [], seams[0]["shard_start"]
+    """seam_resolve_kernel: ("ok", ext cuts, c_rank) where the rank's true cuts
+    are ext + [spec cuts >= c_rank], or ("resync", failing rank, its true entry
+    cut) when some seam did not converge inside its window (every rank checks
+    every seam, so all ranks agree on another exchange round)."""
+    mine = ([], seams[rank]["shard_start"])
     entry = seams[0]["exit_cut"]
-    for r in range(1, rank + 1):
+    for r in range(1, len(seams)):
         s = seams[r]
-        L, PE = s["total"], s["window_end"]
-        is_last = PE == L
-        x, j, ext, c = entry, 0, [], None
-        cutset = set(s["cuts"])
-        if x == s["shard_start"] or s["shard_len"] == 0:
+        ext, c = [], None
+        if s["flags"] & SEAM_REWALKED:
+            if entry == s["entry"]:
+                c = 0
+        elif entry == s["shard_start"] or s["shard_len"] == 0:
             c = s["shard_start"]
         else:
+            L, PE = s["total"], s["window_end"]
+            is_last = PE == L
+            x, j = entry, 0
+            cutset = set(s["cuts"])
             while True:
                 if is_last and x >= L:
                     c = x
@@ -102,13 +126,12 @@ def resolve(seams, rank, mn, mx):
                     ext.append(nx)
                 x = nx
         if c is None:
-            raise RuntimeError(f"seam {r} did not converge inside its window")
+            return "resync", r, entry
         if r == rank:
-            return ext, c
+            mine = (ext, c)
         entry = s["exit_cut"] if s["shard_len"] else entry
-    raise AssertionError
+    return ("ok",) + mine
 
 
-def rank_cuts(seams, rank, spec_cuts, mn, mx):
-    ext, c = resolve(seams, rank, mn, mx)
-    return np.array(ext + [x for x in spec_cuts if x >= c], dtype=np.uint64)
+def rank_cuts(ext, c, spec_cuts):
+    return np.array(list(ext) + [x for x in spec_cuts if x >= c], dtype=np.uint64)

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.lib().dsx_abi_version() == 1
+    assert _lib.lib().dsx_abi_version() == 2
 
 
 @pytest.mark.parametrize("args,code,msg", [
@@ -66,3 +66,10 @@ def test_no_gpu_context_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(_lib.DsxError):
         _lib.Context(0)
+
+
+def test_seam_record_layout():
+    """dsx_seam_t is exchanged as raw bytes between ranks: the ctypes mirror
+    has the C layout (static_assert in dsx_api.cpp)."""
+    assert ctypes.sizeof(_lib.Seam) == 7 * 8 + 4 * 4 + 8 * (1024 + 1024)
+    assert _lib.Seam.cands.offset == 7 * 8 + 4 * 4

@@ -299,3 +299,70 @@ def test_chunk_ids_default_chunking(dctx):
     want = [hashlib.new("sha512_256", buf[s:e]).digest()
             for s, e in zip(starts.tolist(), ends.tolist())]
     assert got == want
+
+
+# ---------------------------------------------------------------- multi-GPU seams
+def _compose_shard(kind):
+    if kind == "random":
+        return o.synth_uniform(21, 0, 12 << 20)
+    r2 = o.synth_uniform(23, 0, 4 * MAX)
+    head = o.synth_uniform(24, 0, 3 * MAX + 12345)
+    # a zero run far longer than the 32*max seam window across the shard
+    # boundaries, entered off the max grid: owners must re-walk (DSX_E_RESYNC)
+    return np.concatenate([head, np.zeros(100 * MAX, np.uint8), r2])
+
+
+@pytest.mark.parametrize("kind,world,dev", [("random", 3, False), ("random", 4, True),
+                                            ("seam-zero-run", 2, False),
+                                            ("seam-zero-run", 4, True)])
+def test_shard_protocol_single_process(kind, world, dev):
+    """dsx_shard_local / dsx_shard_resolve for `world` ranks simulated in one
+    process (one context per rank, records exchanged by hand, host or device
+    records): the concatenated per-rank lists equal the sequential chunker."""
+    import torch
+    import desync_amd
+    from desync_amd import _lib, shard
+    L = _lib.lib()
+    data = _compose_shard(kind)
+    total = data.size
+    span = total // world
+    t = torch_dev(data)
+    p = desync_amd.Params(MIN, AVG, MAX)
+    ctxs = [_lib.Context(0) for _ in range(world)]
+    geo = [(r * span, span if r < world - 1 else total - r * span) for r in range(world)]
+    if dev:
+        recs = [torch.empty(shard.SEAM_BYTES, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        ptr = [x.data_ptr() for x in recs]
+    else:
+        recs = [_lib.Seam() for _ in range(world)]
+        ptr = [ctypes.addressof(x) for x in recs]
+    sflag = _lib.DSX_SEAM_DEVICE if dev else 0
+    for r, (start, length) in enumerate(geo):
+        _lib.check(L.dsx_shard_local(ctxs[r].h, ctypes.c_void_p(t.data_ptr() + start),
+                                     64 if r else 0, start, length, total, ctypes.byref(p.c),
+                                     ctypes.c_void_p(ptr[r]), sflag), ctxs[r].h)
+    outs = [np.empty(length // MIN + 4 + 1024, np.uint64) for _, length in geo]
+    counts = [ctypes.c_uint64() for _ in range(world)]
+    rounds = 0
+    while True:
+        rounds += 1
+        assert rounds <= world + 1
+        if dev:
+            allrec = torch.cat(recs)
+            torch.cuda.synchronize()
+            aptr = allrec.data_ptr()
+        else:
+            allrec = (_lib.Seam * world)(*recs)
+            aptr = ctypes.addressof(allrec)
+        rcs = [L.dsx_shard_resolve(ctxs[r].h, ctypes.c_void_p(aptr), world, r,
+                                   ctypes.c_void_p(ptr[r]), outs[r].ctypes.data, outs[r].size,
+                                   ctypes.byref(counts[r]), sflag) for r in range(world)]
+        if all(rc == 0 for rc in rcs):
+            break
+        assert all(rc == _lib.DSX_E_RESYNC for rc in rcs), rcs
+    got = np.concatenate([outs[r][:counts[r].value] for r in range(world)])
+    assert np.array_equal(got, o.chunk_stream(data, MIN, AVG, MAX))
+    if kind == "seam-zero-run":
+        assert rounds > 1
+    for c in ctxs:
+        c.close()

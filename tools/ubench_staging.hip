@@ -102,6 +102,80 @@ __global__ __launch_bounds__(WAVES * 64) void k_dma(const uint8_t* base, uint32_
   if (acc == 0x12345678) out[0] = acc;
 }
 
+// k_dma + a contiguous L2 prefetch: every PFB batches the wave touches, with
+// one buffer_load_dword per lane into a dummy LDS slot, the next PFK KiB of
+// 64/(PFK*16) lane segments per instruction (one dword per 64 B half-line), so
+// DRAM sees PFK KiB contiguous bursts instead of 64 interleaved ROWB-byte rows.
+template <int ROWB, int NB, int WAVES, int PFK, int AHEAD>
+__global__ __launch_bounds__(WAVES * 64) void k_dma_pf(const uint8_t* base, uint32_t S, uint32_t nregions, uint64_t len, uint32_t* out) {
+  constexpr int BUF = 64 * ROWB;
+  constexpr int NI = BUF / 1024;
+  constexpr int LPS = PFK * 16;          // lanes per segment chunk (one per 64 B)
+  constexpr int SPI = 64 / LPS;          // segments per prefetch instruction
+  constexpr int NPI = 64 / SPI;          // prefetch instructions per PFK KiB of all 64 segments
+  __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * NB * BUF + WAVES * 256];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint8_t* stage = lds + wave * NB * BUF;
+  const uint32_t stage_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)stage);
+  const uint32_t dummy_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(lds + WAVES * NB * BUF + wave * 256));
+  uint32_t acc = 0;
+  const uint32_t B = S / ROWB;
+  uint32_t roff[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const uint32_t u = i * 64 + lane;
+    roff[i] = (u / (ROWB / 16)) * S + (u % (ROWB / 16)) * 16;
+  }
+  const uint32_t pf_seg = lane / LPS, pf_off = (lane % LPS) * 64;
+  for (uint32_t region = blockIdx.x * WAVES + wave; region < nregions; region += gridDim.x * WAVES) {
+    const uint64_t rp = (uint64_t)(uintptr_t)(base + (uint64_t)region * 64 * S);
+    u32x4 rs;
+    rs.x = __builtin_amdgcn_readfirstlane((uint32_t)rp);
+    rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(rp >> 32) & 0xFFFF);
+    rs.z = 64u * S;
+    rs.w = 0x00020000u;
+    auto issue = [&](uint32_t b) {
+      const uint32_t dst = stage_lds + (b % NB) * BUF;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) dma16(rs, b < B ? roff[i] + b * ROWB : 0xFFFFFFF0u, dst + i * 1024);
+    };
+    // prefetch instruction pi: chunk pi / NPI (PFK KiB of SPI segments); issued
+    // as Q per batch (a dummy out-of-range load once AHEAD chunks ahead) so
+    // that vmcnt counting stays exact
+    constexpr int Q = (NPI * ROWB + PFK * 1024 - 1) / (PFK * 1024) + 1;
+    uint32_t pi = 0;
+    auto prefetch1 = [&](uint32_t cur_chunk) {
+      const uint32_t c = pi / NPI, i = pi % NPI;
+      uint32_t vo = 0xFFFFFFF0u;
+      if (c <= cur_chunk + AHEAD) {
+        const uint32_t o = c * PFK * 1024u + pf_off;
+        if (o < S) vo = (i * SPI + pf_seg) * S + o;
+        ++pi;
+      }
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(vo), "s"(dummy_lds), "s"(rs) : "memory");
+    };
+    for (int b = 0; b < NB - 1; ++b) {
+      issue(b);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) prefetch1(0);
+    }
+    for (uint32_t b = 0; b < B; ++b) {
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"((NB - 2) * (NI + Q) + Q) : "memory");
+      const uint4* src = (const uint4*)(stage + (b % NB) * BUF + lane * ROWB);
+#pragma unroll
+      for (int c = 0; c < ROWB / 16; ++c) { uint4 v = src[c]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(b + NB - 1);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) prefetch1((b * ROWB) / (PFK * 1024u));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (acc == 0x12345678) out[0] = acc;
+}
+
 int main() {
   const uint64_t len = 1ull << 30;
   uint8_t* d; uint32_t* o;
@@ -119,19 +193,26 @@ int main() {
     printf("%-40s %8.3f ms  %7.0f GB/s  %s\n", name, ms / it, len / (ms / it * 1e-3) / 1e9, hipGetErrorString(hipGetLastError()));
   };
   timeit("coalesced copy-read", [&] { k_copy<<<ncu * 8, 256>>>((const uint4*)d, len / 16, o); });
-  const uint32_t S = 8208;
+  const uint32_t S = 8256;  // multiple of 96 and 192 (43 x 192)
   const uint32_t nreg = (uint32_t)((len + 64ull * S - 1) / (64ull * S)) - 1;  // keep in bounds
-  timeit("dma rows48 nb4 8w (current)", [&] { k_dma<48, 4, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
   timeit("dma rows96 nb3 8w", [&] { k_dma<96, 3, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
   timeit("dma rows96 nb2 8w", [&] { k_dma<96, 2, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("dma rows96 nb3 6w", [&] { k_dma<96, 3, 6><<<ncu, 384>>>(d, S, nreg, len, o); });
-  timeit("dma rows144 nb2 8w", [&] { k_dma<144, 2, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("dma rows144 nb2 6w", [&] { k_dma<144, 2, 6><<<ncu, 384>>>(d, S, nreg, len, o); });
-  timeit("dma rows144 nb3 4w", [&] { k_dma<144, 3, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
-  timeit("dma rows192 nb2 4w", [&] { k_dma<192, 2, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
-  timeit("dma rows240 nb2 4w", [&] { k_dma<240, 2, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
-  timeit("dma rows96 nb4 4w", [&] { k_dma<96, 4, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
-  timeit("dma rows48 nb4 4w", [&] { k_dma<48, 4, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
-  timeit("dma rows48 nb8 4w", [&] { k_dma<48, 8, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  timeit("dma rows192 nb2 6w", [&] { k_dma<192, 2, 6><<<ncu, 384>>>(d, S, nreg, len, o); });
+  timeit("dma rows192 nb3 4w", [&] { k_dma<192, 3, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
+  timeit("pf rows96 nb3 8w pfk1 a2", [&] { k_dma_pf<96, 3, 8, 1, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("pf rows96 nb3 8w pfk1 a4", [&] { k_dma_pf<96, 3, 8, 1, 4><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("pf rows96 nb3 8w pfk2 a2", [&] { k_dma_pf<96, 3, 8, 2, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("pf rows96 nb3 8w pfk4 a1", [&] { k_dma_pf<96, 3, 8, 4, 1><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("pf rows96 nb3 8w pfk4 a2", [&] { k_dma_pf<96, 3, 8, 4, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("pf rows96 nb2 8w pfk2 a2", [&] { k_dma_pf<96, 2, 8, 2, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
+  timeit("pf rows192 nb2 6w pfk2 a2", [&] { k_dma_pf<192, 2, 6, 2, 2><<<ncu, 384>>>(d, S, nreg, len, o); });
+  for (uint32_t S2 : {1056u, 2064u, 4128u}) {
+    const uint32_t nr2 = (uint32_t)((len + 64ull * S2 - 1) / (64ull * S2)) - 1;
+    char nm[64];
+    snprintf(nm, sizeof nm, "dma rows96 nb3 8w S=%u", S2);
+    timeit(nm, [&] { k_dma<96, 3, 8><<<ncu, 512>>>(d, S2, nr2, len, o); });
+    snprintf(nm, sizeof nm, "pf rows96 nb3 8w pfk1 a2 S=%u", S2);
+    timeit(nm, [&] { k_dma_pf<96, 3, 8, 1, 2><<<ncu, 512>>>(d, S2, nr2, len, o); });
+  }
   return 0;
 }

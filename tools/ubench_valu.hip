@@ -53,6 +53,9 @@ KERNEL(k_lshr, "v_lshrrev_b32 %0, 3, %0")
 KERNEL(k_and, "v_and_b32 %0, %0, %1")
 KERNEL(k_cvt_ubyte, "v_cvt_f32_ubyte1 %0, %0")
 
+KERNEL(k_lshl_add, "v_lshl_add_u32 %0, %0, 1, %1")
+KERNEL(k_bfe, "v_bfe_u32 %0, %0, 8, 8")
+
 // compare into SGPR pairs + s_or accumulate (ballot pattern)
 __global__ void k_cmp(uint32_t* out, uint32_t seed) {
   uint32_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
@@ -97,6 +100,41 @@ __global__ void k_chain(uint32_t* out, uint32_t seed) {
   if (r == 0x12345679u + c) out[0] = r;
 }
 
+// N independent dependent chains (alignbit -> xor per step), 8 steps per iteration
+template <int N>
+__global__ void k_chainN(uint32_t* out, uint32_t seed) {
+  uint32_t a[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) a[j] = threadIdx.x ^ (seed + j);
+  uint32_t b = seed * 3u + 1u;
+  for (int i = 0; i < ITER / N; ++i) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) asm volatile("v_alignbit_b32 %0, %0, %0, 31" : "+v"(a[j]));
+#pragma unroll
+      for (int j = 0; j < N; ++j) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+    }
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) r ^= a[j];
+  if (r == 0x12345679u) out[0] = r;
+}
+
+// v_mad_u64_u32 (64-bit result; the low half is h*inv + c)
+__global__ void k_mad64(uint32_t* out, uint32_t seed) {
+  uint64_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t b = seed * 3u + 1u;
+  uint64_t c = seed * 5u + 7u;
+  for (int i = 0; i < ITER; ++i) {
+#define M64(x) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(x) : "v"((uint32_t)x), "v"(b), "v"(c) : "vcc");
+    M64(a0) M64(a1) M64(a2) M64(a3) M64(a4) M64(a5) M64(a6) M64(a7)
+  }
+  uint64_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+  if (r == 0x12345679u) out[0] = (uint32_t)r;
+}
+
 int main() {
   uint32_t* o;
   CHK(hipMalloc(&o, 64));
@@ -115,9 +153,12 @@ int main() {
             {"v_sad_u32", k_sad, 8},       {"v_mul_lo_u32", k_mullo, 8},    {"v_mul_hi_u32", k_mulhi, 8},
             {"v_cmp_e64+s_or", k_cmp, 8},  {"v_mov_b32_sdwa", k_sdwa_mov, 8}, {"v_or_b32_sdwa", k_sdwa_or, 8},
             {"v_min_u32", k_min, 8},       {"v_sub_u32", k_sub, 8},         {"v_lshrrev_b32", k_lshr, 8},
-            {"v_and_b32", k_and, 8},       {"v_cvt_f32_ubyte1", k_cvt_ubyte, 8},  {"v_pk_fma_f32", k_pkfma, 8},    {"chain alignbit+xor", k_chain, 8}};
+            {"v_and_b32", k_and, 8},       {"v_cvt_f32_ubyte1", k_cvt_ubyte, 8},  {"v_pk_fma_f32", k_pkfma, 8},    {"chain alignbit+xor", k_chain, 8},
+            {"v_lshl_add_u32", k_lshl_add, 8}, {"v_bfe_u32", k_bfe, 8},
+            {"chain1 (alignbit,xor)", k_chainN<1>, 8}, {"chain2", k_chainN<2>, 8}, {"chain4", k_chainN<4>, 8},
+            {"chain8", k_chainN<8>, 8}, {"v_mad_u64_u32", k_mad64, 8}};
   printf("clock attr %d kHz\n", clk_khz);
-  for (int wps : {2}) {
+  for (int wps : {1, 2, 4}) {
     for (auto& k : ks) {
       const int threads = 64 * 4 * wps;  // one block per CU, wps waves per SIMD
       hipLaunchKernelGGL(k.f, dim3(ncu), dim3(threads), 0, 0, o, 1u);
