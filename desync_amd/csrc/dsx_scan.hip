@@ -176,11 +176,10 @@ __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t
 #pragma unroll
     for (int i = 0; i < SUB; ++i) {
       const int k = j * SUB + i;
-      // rotl1(h) ^ (T[in] ^ Trot[out]); the asm fence keeps the compiler from
-      // re-associating the second xor back onto the h chain
-      uint32_t x = (uint32_t)L[j & 1][i] ^ ring[k];
-      asm("" : "+v"(x));
-      h = __builtin_amdgcn_alignbit(h, h, 31) ^ x;
+      // rotl1(h) ^ T[in] ^ Trot[out]: one v_alignbit + one three-input
+      // v_bitop3_b32 (xor3, gfx950)
+      h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31),
+                                      (uint32_t)L[j & 1][i], ring[k], 0x96);
       ring[k] = (uint32_t)(L[j & 1][i] >> 32);
       if constexpr (kTest && MODE == 2) t[i] = mode2_t_mad(h, tc.inv, (uint64_t)tc.tadd);
       else if constexpr (kTest) m[i] = __ballot(is_cand<MODE>(h, tc));
