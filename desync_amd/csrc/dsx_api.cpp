@@ -30,6 +30,8 @@ template <class H>
 __global__ void digest_kernel(DigestArgs a);
 template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ void scan_kernel(ScanArgs a);
+template <int MODE, int VARIANT, int W, int SUB>
+__global__ void scanl_kernel(ScanArgs a);
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);
@@ -104,6 +106,11 @@ struct dsx_ctx {
   int prefetch_batches = 0;           // DSX_PREFETCH: L2 prefetch distance in DMA batches (0 = off)
   int regions_per_slot = 1;           // DSX_REGIONS_PER_SLOT: scan work units per wave slot
   int scan_cfg = 0;                   // DSX_SCAN_CFG: index into kCfg* (waves, rounds/batch, LDS buffers)
+  bool scan_line = true;              // DSX_SCAN_LINE=0: 96-B-row scan_kernel instead of scanl_kernel
+  int scanl_waves = 8;                // DSX_SCANL_WAVES: 8 or 12
+  int scanl_sub = 8;                  // DSX_SCANL_SUB: 4 or 8 (12-wave kernel)
+  uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
+  uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
   DevBuf<uint32_t> lane_slot;
@@ -316,6 +323,11 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
+  if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
+  if (const char* v = getenv("DSX_SCANL_WAVES")) c->scanl_waves = atoi(v) == 12 ? 12 : 8;
+  if (const char* v = getenv("DSX_SCANL_SUB")) c->scanl_sub = atoi(v) == 4 ? 4 : 8;
+  if (const char* v = getenv("DSX_LANE_TARGET"))
+    c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
     const long lb = atol(v);
     if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
@@ -424,13 +436,36 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   // scan configs: {waves per workgroup, rounds per DMA batch}
   static const int kCfgWaves[6] = {8, 12, 16, 12, 8, 16};
   static const int kCfgBR[6] = {2, 1, 1, 2, 2, 2};
-  const int W = kCfgWaves[c->scan_cfg];
+  // line-aligned scan (scanl_kernel) unless disabled, on the dense path, or
+  // when the grid origin P - delta would precede position 0
+  const uint32_t delta = (uint32_t)((uintptr_t)d_piece & (kLine - 1));
+  const bool line = c->scan_line && !cc.dense && P >= delta;
+  const int W = line ? c->scanl_waves : kCfgWaves[c->scan_cfg];
   const int cfgBR = kCfgBR[c->scan_cfg];
   const uint64_t slots_total = (uint64_t)c->ncu * W;  // wave slots
+  const uint64_t span = line ? len + delta : len;       // grid bytes
   uint32_t S, LS;
+  uint32_t batches;
   if (cc.dense) {
     S = kDenseS;
     LS = S;
+  } else if (line) {
+    // S = 384*m: about regions_per_slot regions per wave slot
+    const uint64_t lanes_min = slots_total * 64 * (uint64_t)c->regions_per_slot;
+    const uint64_t per_lane = (span + lanes_min - 1) / lanes_min;
+    const uint64_t rounds_needed = (per_lane + kLineLaneMax - 1) / kLineLaneMax;
+    const uint64_t s = (span + rounds_needed * lanes_min - 1) / (rounds_needed * lanes_min);
+    uint64_t m = (s + 3 * kLine - 1) / (3 * kLine);
+    // lane segments longer than the target lose HBM efficiency (lane stride
+    // 33 KB: 4.85 TB/s staging vs 6.24 TB/s at 8448 B, tools/ubench_staging.hip);
+    // bigger pieces take more regions per wave slot from the work queue
+    m = std::min<uint64_t>(m, c->lane_target / (3 * kLine));
+    m = std::max<uint64_t>(1, std::min<uint64_t>(m, kLineLaneMax / (3 * kLine)));
+    S = (uint32_t)(3 * kLine * m);
+    if (c->lane_bytes_override && c->lane_bytes_override % (3 * kLine) == 0 &&
+        c->lane_bytes_override <= kLineLaneMax)
+      S = c->lane_bytes_override;
+    LS = kLaneSlots;
   } else {
     // about regions_per_slot regions per wave slot (dynamic queue balances
     // them), more if a lane segment would exceed kMaxLaneBytes
@@ -448,9 +483,9 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     S = (uint32_t)s;
     LS = kLaneSlots;
   }
-  const uint32_t batches = (S / kRound + 1) / (uint32_t)cfgBR;
+  batches = line ? S / (3 * kLine) : (S / kRound + 1) / (uint32_t)cfgBR;
   const uint64_t region_bytes = 64ull * S;
-  const uint64_t nregions = len == 0 ? 0 : (len + region_bytes - 1) / region_bytes;
+  const uint64_t nregions = len == 0 ? 0 : (span + region_bytes - 1) / region_bytes;
   const uint64_t nlanes = nregions * 64;
   uint32_t rcap;
   if (cc.dense) {
@@ -490,6 +525,16 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   sa.queue_next = c->overflow.p + 2 + ((seq + 1) & 1);
   sa.state_init = c->init_pending ? (void*)c->state.p : nullptr;
   sa.init_carry = c->init_carry;
+  if (line) {
+    // region 0's descriptor: the warm-up line unless it would start before
+    // the readable bytes (then the 16-B step at or below base - min(halo, 48))
+    const uint64_t hmin = std::min<uint64_t>(halo, kRound);
+    sa.delta = delta;
+    sa.shift0 = halo >= (uint64_t)delta + kLine
+                    ? 0u
+                    : (uint32_t)(16 * (((uint64_t)kLine + delta - hmin) / 16));
+  }
+  c->last_grid_P = line ? P - delta : P;
   c->init_pending = false;
   const uint32_t pi = c->npiece_call++;
   while (c->pev.size() < 3 * (size_t)(pi + 1)) {
@@ -518,7 +563,26 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     else                                                                                   \
       hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
   } while (0)
-    switch (c->scan_cfg) {
+#define DSX_LAUNCHL(WV, SUB)                                                              \
+  do {                                                                                    \
+    if (c->variant == 1)                                                                  \
+      hipLaunchKernelGGL((scanl_kernel<2, 1, WV, SUB>), g, b, 0, c->stream, sa);          \
+    else if (c->variant == 3)                                                             \
+      hipLaunchKernelGGL((scanl_kernel<2, 3, WV, SUB>), g, b, 0, c->stream, sa);          \
+    else if (c->variant == 4)                                                             \
+      hipLaunchKernelGGL((scanl_kernel<2, 4, WV, SUB>), g, b, 0, c->stream, sa);          \
+    else if (mode == 2)                                                                   \
+      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB>), g, b, 0, c->stream, sa);          \
+    else if (mode == 1)                                                                   \
+      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB>), g, b, 0, c->stream, sa);          \
+    else                                                                                  \
+      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB>), g, b, 0, c->stream, sa);          \
+  } while (0)
+    if (line) {
+      if (W == 12 && c->scanl_sub == 4) DSX_LAUNCHL(12, 4);
+      else if (W == 12) DSX_LAUNCHL(12, 8);
+      else DSX_LAUNCHL(8, 8);
+    } else switch (c->scan_cfg) {
       case 1: DSX_LAUNCH(1, 2, 12, 4, false); break;
       case 2: DSX_LAUNCH(1, 2, 16, 4, false); break;
       case 3: DSX_LAUNCH(2, 1, 12, 8, false); break;
@@ -529,6 +593,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
         else DSX_LAUNCH(2, 2, 8, 8, false);
     }
 #undef DSX_LAUNCH
+#undef DSX_LAUNCHL
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));
@@ -539,7 +604,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.chain.L = cc.L;
   ta.chain.PE = P + len;
   ta.chain.is_last = is_last ? 1u : 0u;
-  ta.pc.P = P;
+  ta.pc.P = c->last_grid_P;  // region r covers (P' + r*RB, P' + (r+1)*RB]
   ta.pc.RB = region_bytes;
   ta.pc.nregions = (uint32_t)nregions;
   ta.pc.region_cap = rcap;
@@ -1135,7 +1200,7 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags) {
       if (off == 0) {
         // the window candidates come from the first piece's region lists
         PieceCands pc{};
-        pc.P = sh.start;
+        pc.P = c->last_grid_P;
         pc.RB = c->last_region_bytes;
         pc.nregions = c->last_nregions;
         pc.region_cap = c->last_region_cap;

@@ -65,7 +65,17 @@ struct ScanArgs {
   uint32_t* queue_next;  // the next piece's queue counter: zeroed here
   void* state_init;      // if non-null: DevState to initialise (first piece of a call)
   uint64_t init_carry;
+  // line-aligned scan (scanl_kernel): the lane grid starts at base - delta,
+  // the 128-B line holding base[0]; region 0's descriptor starts shift0 bytes
+  // into its warm-up line (bytes before it read as zeros)
+  uint32_t delta;
+  uint32_t shift0;
 };
+
+// line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches
+// of one 128-B line per lane, so the ring phase repeats), offsets in u16
+constexpr int kLine = 128;
+constexpr uint32_t kLineLaneMax = 384u * 170u;  // 65280
 
 // Sentinel for "successor depends on bytes beyond the piece" (non-final piece).
 constexpr uint64_t kUndet = ~0ull;

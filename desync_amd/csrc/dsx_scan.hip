@@ -145,19 +145,22 @@ __device__ __forceinline__ void lookups_landed(uint64_t (&L)[SUB]) {
   }
 }
 
-template <bool TEST, int MODE, int VARIANT, int SUB>
-__device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t (&ring)[48],
-                                        const uint8_t* __restrict__ tbl, uint32_t slot8,
-                                        const TestConsts& tc, uint32_t lane, uint32_t obase,
-                                        uint32_t& cnt, uint32_t (&ereg)[kHitRegs],
-                                        uint32_t* __restrict__ myslots, uint32_t lane_slots) {
+// Hash bytes [0, NB) of w (byte i is byte i&3 of w[i>>2]); byte i uses ring
+// slot (PH + i) % 48, so spans of any length keep the ring static.
+template <int NB, int PH, bool TEST, int MODE, int VARIANT, int SUB>
+__device__ __forceinline__ void hash_span(const uint32_t* w, uint32_t& h, uint32_t (&ring)[48],
+                                          const uint8_t* __restrict__ tbl, uint32_t slot8,
+                                          const TestConsts& tc, uint32_t lane, uint32_t obase,
+                                          uint32_t& cnt, uint32_t (&ereg)[kHitRegs],
+                                          uint32_t* __restrict__ myslots, uint32_t lane_slots) {
+  static_assert(NB % SUB == 0 && NB % 4 == 0, "span shape");
   if constexpr (VARIANT == 3) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) h ^= w[k];
+    for (int k = 0; k < NB / 4; ++k) h ^= w[k];
     asm volatile("" ::"v"(h));
     return;
   }
-  constexpr int NSG = kRound / SUB;
+  constexpr int NSG = NB / SUB;
   uint64_t L[2][SUB];  // {T[in], rotl16(T[in])} lookups, double-buffered
   auto issue = [&](int j) {
 #pragma unroll
@@ -178,9 +181,10 @@ __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t
       const int k = j * SUB + i;
       // rotl1(h) ^ T[in] ^ Trot[out]: one v_alignbit + one three-input
       // v_bitop3_b32 (xor3, gfx950)
+      const int rk = (PH + k) % 48;
       h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31),
-                                      (uint32_t)L[j & 1][i], ring[k], 0x96);
-      ring[k] = (uint32_t)(L[j & 1][i] >> 32);
+                                      (uint32_t)L[j & 1][i], ring[rk], 0x96);
+      ring[rk] = (uint32_t)(L[j & 1][i] >> 32);
       if constexpr (kTest && MODE == 2) t[i] = mode2_t_mad(h, tc.inv, (uint64_t)tc.tadd);
       else if constexpr (kTest) m[i] = __ballot(is_cand<MODE>(h, tc));
     }
@@ -227,6 +231,16 @@ __device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t
     compute(j);
     __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+template <bool TEST, int MODE, int VARIANT, int SUB>
+__device__ __forceinline__ void round48(const uint32_t* w, uint32_t& h, uint32_t (&ring)[48],
+                                        const uint8_t* __restrict__ tbl, uint32_t slot8,
+                                        const TestConsts& tc, uint32_t lane, uint32_t obase,
+                                        uint32_t& cnt, uint32_t (&ereg)[kHitRegs],
+                                        uint32_t* __restrict__ myslots, uint32_t lane_slots) {
+  hash_span<kRound, 0, TEST, MODE, VARIANT, SUB>(w, h, ring, tbl, slot8, tc, lane, obase, cnt,
+                                                 ereg, myslots, lane_slots);
 }
 
 // BR rounds per LDS-DMA batch (rows of BR*48 B per lane), NBUF LDS buffers per
@@ -502,6 +516,249 @@ DSX_SCAN_INST(1, 2, 16, 4, false)
 DSX_SCAN_INST(2, 1, 12, 8, false)
 DSX_SCAN_INST(2, 1, 8, 8, false)
 DSX_SCAN_INST(2, 1, 16, 4, false)
+
+// ---------------------------------------------------------------------------
+// scanl_kernel -- the line-aligned scan (default path).
+//
+// Same per-byte work as scan_kernel, but every HBM request is a whole 128-B
+// line fetched once: lane segments of S = 384*m bytes start on line
+// boundaries of the grid base - delta, and each DMA batch is ONE line per
+// lane (8 wave instructions, each 8 lanes x 128 B = 8 whole lines).
+// scan_kernel's 96-B rows straddle lines, and 18 % of those lines were
+// fetched twice from HBM (TCC_EA0_RDREQ_128B = 1.18 x the input bytes,
+// tools/pmc_tcc.sh): the L2 dropped a half-used line before the row next to
+// it arrived.  The warm-up is the last 48 bytes of the line before the
+// segment (128/S extra reads).  One LDS staging line per lane (8 KiB per
+// wave): a batch is copied to registers, then the next batch's DMA is issued
+// at once, so it lands while this one is hashed.  A batch of 128 B is three
+// ring phases apart from the next (128 = 2*48 + 32), so the steady-state loop
+// runs three batches with phases 0, 32, 16.
+// ---------------------------------------------------------------------------
+template <int MODE, int VARIANT, int W, int SUB>
+__global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
+  constexpr int NC = kLine / 16;             // 16-B chunks per lane row
+  constexpr int NI = kWave * kLine / 1024;   // DMA wave instructions per batch
+  constexpr int STG = kWave * kLine;         // staging bytes per wave
+  constexpr int LDSB = kTableBytes + W * STG;
+  constexpr int NT = W * kWave;
+  static_assert(LDSB <= kScanLds, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
+
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *a.overflow_next = 0u;
+    *a.queue_next = 0u;
+    if (a.state_init) {
+      uint64_t* st = (uint64_t*)a.state_init;
+      st[0] = a.init_carry;
+      st[1] = 0;
+      st[2] = 0;
+      st[3] = 0;
+      st[4] = 0;
+      st[5] = 0;
+    }
+  }
+  if constexpr (VARIANT == 4) {
+    for (int e = threadIdx.x; e < W * STG / 4; e += NT)
+      reinterpret_cast<uint32_t*>(lds + kTableBytes)[e] = 0u;
+  }
+  for (int e = threadIdx.x; e < 256 * 32; e += NT) {
+    const uint32_t v = kT[e >> 5];
+    uint2 t;
+    t.x = v;
+    t.y = __builtin_amdgcn_alignbit(v, v, 16);
+    *reinterpret_cast<uint2*>(lds + (e >> 5) * 256 + (e & 31) * 8) = t;
+  }
+  __syncthreads();
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t slot8 = (lane & 31u) * 8u;
+  uint8_t* stage = lds + kTableBytes + wave * STG;
+  const uint32_t stage_lds =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)stage);
+  const uint32_t S = a.lane_bytes;
+  const uint32_t M = a.batches;        // loop trips of 3 batches: S = 3*128*M
+  const uint32_t NB = 3u * M + 1u;     // batches per lane, warm-up line included
+  const uint64_t RB = 64ull * S;
+
+  // DMA geometry: instruction i, lane j -> 16-B unit u = 64i + j of the wave's
+  // 64 x 128 B image: row u/8, physical chunk u%8.  Row r stores logical
+  // chunk c at physical (c + rot(r)) % 8 with rot(r) = (r >> 1) % 8, which
+  // makes the ds_read_b128 row reads conflict-free (each 16-lane group covers
+  // the 16 distinct {row parity, chunk} bank quads).
+  uint32_t dma_off[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const uint32_t u = (uint32_t)i * 64u + lane;
+    const uint32_t row = u / (uint32_t)NC, phys = u % (uint32_t)NC;
+    const uint32_t c = (phys + (uint32_t)NC - ((row >> 1) % (uint32_t)NC)) % (uint32_t)NC;
+    dma_off[i] = row * S + c * 16u;
+  }
+  const uint32_t rot = (lane >> 1) % (uint32_t)NC;
+  TestConsts tcv = a.tc;
+  asm volatile("" : "+v"(tcv.c0));
+  asm volatile("" : "+v"(tcv.madc));
+  if constexpr (MODE == 2) asm volatile("" : "+v"(tcv.inv));
+
+  // Region r's descriptor starts at its warm-up line (grid-relative
+  // r*RB - 128), shifted by shift0 for region 0 so it never precedes the
+  // readable bytes; offsets below the base wrap out of range and read 0.
+  auto desc_of = [&](uint32_t region, u32x4& rsrc, uint32_t& sh) {
+    sh = region == 0 ? a.shift0 : 0u;
+    const int64_t rel = (int64_t)region * (int64_t)RB - (int64_t)a.delta - kLine + (int64_t)sh;
+    const uint64_t rp = (uint64_t)(uintptr_t)(a.base + rel);
+    const uint64_t nrec64 = (uint64_t)((int64_t)a.len - rel);
+    const uint32_t nrec = nrec64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nrec64;
+    rsrc.x = __builtin_amdgcn_readfirstlane((uint32_t)rp);
+    rsrc.y = __builtin_amdgcn_readfirstlane((uint32_t)(rp >> 32) & 0xFFFFu);
+    rsrc.z = __builtin_amdgcn_readfirstlane(nrec);
+    rsrc.w = 0x00020000u;
+  };
+  // batch b of every lane (b = 0: warm-up line); b >= NB: out-of-range loads
+  // (zeros) so every batch is NI instructions
+  auto issue = [&](const u32x4& rsrc, uint32_t sh, uint32_t b) {
+    if constexpr (VARIANT == 4) return;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t vo = (b < NB) ? dma_off[i] + b * (uint32_t)kLine - sh : 0xFFFFFFF0u;
+      dma16(rsrc, vo, stage_lds + (uint32_t)i * 1024u);
+    }
+  };
+
+  uint32_t region = blockIdx.x * W + wave;
+  if (region >= a.nregions) return;
+  u32x4 rsrc;
+  uint32_t sh;
+  desc_of(region, rsrc, sh);
+  uint32_t ticket = 0;
+  if (lane == 0) ticket = atomicAdd(a.queue, 1u);
+  issue(rsrc, sh, 0u);
+
+  while (true) {
+    const uint32_t next = gridDim.x * W + __builtin_amdgcn_readfirstlane(ticket);
+    u32x4 nrsrc = rsrc;
+    uint32_t nsh = 0;
+    if (next < a.nregions) {
+      if (lane == 0) ticket = atomicAdd(a.queue, 1u);
+      desc_of(next, nrsrc, nsh);
+    }
+
+    uint32_t cnt = 0;
+    uint32_t ereg[kHitRegs] = {};
+    const uint64_t gl = (uint64_t)region * 64u + lane;
+    uint32_t* myslots = a.lane_slot + gl * a.lane_slots;
+    uint32_t h = 0;
+    uint32_t ring[48];
+#pragma unroll
+    for (int k = 0; k < 48; ++k) ring[k] = 0;
+    uint32_t w[NC * 4];
+
+    // wait for batch b, copy this lane's row to registers, issue batch b+1
+    // (or the next region's warm-up line) into the freed staging line
+    auto fetch = [&](uint32_t b) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint8_t* my_row = stage + lane * (uint32_t)kLine;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint32_t pc = ((uint32_t)c + rot) % (uint32_t)NC;
+        const uint4 q = *reinterpret_cast<const uint4*>(my_row + pc * 16u);
+        w[4 * c] = q.x;
+        w[4 * c + 1] = q.y;
+        w[4 * c + 2] = q.z;
+        w[4 * c + 3] = q.w;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (b + 1u < NB)
+        issue(rsrc, sh, b + 1u);
+      else
+        issue(nrsrc, nsh, next < a.nregions ? 0u : NB);
+    };
+    fetch(0u);
+    // warm-up: the last 48 bytes before the segment fill the window (no test)
+    hash_span<kRound, 0, false, MODE, VARIANT, SUB>(w + 20, h, ring, lds, slot8, tcv, lane, 0u,
+                                                    cnt, ereg, myslots, 0u);
+    for (uint32_t t = 0; t < M; ++t) {
+      const uint32_t o0 = t * 3u * (uint32_t)kLine;
+      fetch(3u * t + 1u);
+      hash_span<kLine, 0, true, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane, o0, cnt,
+                                                    ereg, myslots, a.lane_slots);
+      fetch(3u * t + 2u);
+      hash_span<kLine, 32, true, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane,
+                                                     o0 + kLine, cnt, ereg, myslots,
+                                                     a.lane_slots);
+      fetch(3u * t + 3u);
+      hash_span<kLine, 16, true, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane,
+                                                     o0 + 2u * kLine, cnt, ereg, myslots,
+                                                     a.lane_slots);
+    }
+
+    // ---- region end: compact the lanes' hits into one sorted region list ----
+    // valid cut offsets o: piece-relative p = lane_p + o in [1, len] and
+    // absolute p >= min_pos (windows reaching before the chain origin)
+    const int64_t lane_p = (int64_t)region * (int64_t)RB + (int64_t)lane * S - (int64_t)a.delta;
+    int64_t lo = 1 - lane_p;
+    const int64_t lo2 = (int64_t)a.min_pos - (int64_t)a.piece_abs - lane_p;
+    lo = lo > lo2 ? lo : lo2;
+    const uint32_t o_min = lo <= 1 ? 1u : (lo > (int64_t)S ? S + 1u : (uint32_t)lo);
+    const int64_t hi = (int64_t)a.len - lane_p;
+    const uint32_t o_max = hi <= 0 ? 0u : (hi >= (int64_t)S ? S : (uint32_t)hi);
+    const uint32_t n = cnt < a.lane_slots + kHitRegs ? cnt : a.lane_slots + kHitRegs;
+    const bool spilled = __ballot(cnt > (uint32_t)kHitRegs) != 0;
+    auto for_each_hit = [&](auto&& f) {
+      auto expand = [&](uint32_t e) {
+        const uint32_t base = e & 0xFFFFu;
+        for (uint32_t bits = e >> 16; bits; bits &= bits - 1u) {
+          const uint32_t o = base + (uint32_t)__builtin_ctz(bits) + 1u;
+          if (o >= o_min && o <= o_max) f(o);
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < kHitRegs; ++q)
+        if ((uint32_t)q < n) expand(ereg[q]);
+      if (spilled)
+        for (uint32_t i = kHitRegs; i < n; ++i) expand(myslots[i - kHitRegs]);
+    };
+    uint32_t keep = 0;
+    for_each_hit([&](uint32_t) { ++keep; });
+    uint32_t incl = keep;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += v;
+    }
+    const uint32_t excl = incl - keep;
+    uint32_t exact = keep;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) exact += __shfl_xor(exact, d, 64);
+    uint32_t* rl = a.region_list + (uint64_t)region * a.region_cap;
+    uint32_t j = 0;
+    for_each_hit([&](uint32_t o) {
+      if (excl + j < a.region_cap) rl[excl + j] = lane * S + o;
+      ++j;
+    });
+    const bool lane_ovf = __ballot(cnt > a.lane_slots + kHitRegs) != 0;
+    if (lane == 0) {
+      a.region_cnt[region] = exact;
+      if (lane_ovf || exact > a.region_cap) atomicAdd(a.overflow, 1u);
+    }
+    if (next >= a.nregions) break;
+    region = next;
+    rsrc = nrsrc;
+    sh = nsh;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+#define DSX_SCANL_INST(W, SUB)                                         \
+  template __global__ void scanl_kernel<0, 0, W, SUB>(ScanArgs);       \
+  template __global__ void scanl_kernel<1, 0, W, SUB>(ScanArgs);       \
+  template __global__ void scanl_kernel<2, 0, W, SUB>(ScanArgs);       \
+  template __global__ void scanl_kernel<2, 1, W, SUB>(ScanArgs);       \
+  template __global__ void scanl_kernel<2, 3, W, SUB>(ScanArgs);       \
+  template __global__ void scanl_kernel<2, 4, W, SUB>(ScanArgs);
+DSX_SCANL_INST(8, 8)
+DSX_SCANL_INST(12, 8)
+DSX_SCANL_INST(12, 4)
 
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1
 // (the plain form of chunker_test.go:190-213).  Diagnostic entry point.

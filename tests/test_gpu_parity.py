@@ -159,6 +159,34 @@ def test_random_avg_sweep(dctx, avg):
     assert np.array_equal(gpu_cut(dctx, data, mn, avg, mx), o.chunk_stream(data, mn, avg, mx))
 
 
+@pytest.mark.parametrize("env", [{"DSX_LANE_TARGET": "384"}, {"DSX_LANE_TARGET": "2304"},
+                                 {"DSX_SCAN_LINE": "0"}, {"DSX_SCAN_VARIANT": "0"}])
+def test_scan_geometries(env, monkeypatch):
+    """The line-aligned scan with short lane segments (many regions per wave
+    slot from the work queue), the 96-B-row scan_kernel, and device pointers
+    off the 128-B line grid: at the blob start (scan_kernel fallback) and
+    inside it (shard pieces: grid origin before the piece start)."""
+    import torch
+    import desync_amd
+    from desync_amd import _lib
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ctx = _lib.Context(0)
+    try:
+        data = o.synth_uniform(31, 0, (24 << 20) + 333)
+        assert np.array_equal(gpu_cut(ctx, data), o.chunk_stream(data, MIN, AVG, MAX))
+        for off in (195, 73, 128):  # blobs starting off (or on) the line grid
+            n = (8 << 20) + off
+            arr = o.synth_uniform(32 + off, 0, n)
+            tt = torch_dev(np.concatenate([np.zeros(off, np.uint8), arr]))
+            got = desync_amd.cut_device(tt.data_ptr() + off, n, MIN, AVG, MAX, ctx=ctx)
+            assert np.array_equal(got, o.chunk_stream(arr, MIN, AVG, MAX)), off
+        # shard pieces at odd positions: the line grid starts before the piece
+        _shard_protocol(o.synth_uniform(33, 0, (6 << 20) + 1001), 3, False)
+    finally:
+        ctx.close()
+
+
 def test_odd_params(dctx):
     """min == avg == max, min = 48, max >> avg."""
     data = o.synth_uniform(6, 0, 3 << 20)
@@ -319,11 +347,16 @@ def test_shard_protocol_single_process(kind, world, dev):
     """dsx_shard_local / dsx_shard_resolve for `world` ranks simulated in one
     process (one context per rank, records exchanged by hand, host or device
     records): the concatenated per-rank lists equal the sequential chunker."""
+    rounds = _shard_protocol(_compose_shard(kind), world, dev)
+    if kind == "seam-zero-run":
+        assert rounds > 1
+
+
+def _shard_protocol(data, world, dev):
     import torch
     import desync_amd
     from desync_amd import _lib, shard
     L = _lib.lib()
-    data = _compose_shard(kind)
     total = data.size
     span = total // world
     t = torch_dev(data)
@@ -362,7 +395,6 @@ def test_shard_protocol_single_process(kind, world, dev):
         assert all(rc == _lib.DSX_E_RESYNC for rc in rcs), rcs
     got = np.concatenate([outs[r][:counts[r].value] for r in range(world)])
     assert np.array_equal(got, o.chunk_stream(data, MIN, AVG, MAX))
-    if kind == "seam-zero-run":
-        assert rounds > 1
     for c in ctxs:
         c.close()
+    return rounds

@@ -176,8 +176,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_dma_pf(const uint8_t* base, uint
   if (acc == 0x12345678) out[0] = acc;
 }
 
-int main() {
-  const uint64_t len = 1ull << 30;
+int main(int argc, char** argv) {
+  const uint64_t len = (argc > 1 ? strtoull(argv[1], nullptr, 10) : 4ull) << 30;
   uint8_t* d; uint32_t* o;
   CHK(hipMalloc(&d, len + 4096)); CHK(hipMalloc(&o, 64));
   CHK(hipMemset(d, 7, len));
@@ -190,29 +190,29 @@ int main() {
     for (int i = 0; i < it; ++i) launch();
     hipEventRecord(e1); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
-    printf("%-40s %8.3f ms  %7.0f GB/s  %s\n", name, ms / it, len / (ms / it * 1e-3) / 1e9, hipGetErrorString(hipGetLastError()));
+    printf("%-44s %8.3f ms  %7.0f GB/s  %s\n", name, ms / it, len / (ms / it * 1e-3) / 1e9, hipGetErrorString(hipGetLastError()));
   };
   timeit("coalesced copy-read", [&] { k_copy<<<ncu * 8, 256>>>((const uint4*)d, len / 16, o); });
-  const uint32_t S = 8256;  // multiple of 96 and 192 (43 x 192)
-  const uint32_t nreg = (uint32_t)((len + 64ull * S - 1) / (64ull * S)) - 1;  // keep in bounds
-  timeit("dma rows96 nb3 8w", [&] { k_dma<96, 3, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("dma rows96 nb2 8w", [&] { k_dma<96, 2, 8><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("dma rows192 nb2 6w", [&] { k_dma<192, 2, 6><<<ncu, 384>>>(d, S, nreg, len, o); });
-  timeit("dma rows192 nb3 4w", [&] { k_dma<192, 3, 4><<<ncu, 256>>>(d, S, nreg, len, o); });
-  timeit("pf rows96 nb3 8w pfk1 a2", [&] { k_dma_pf<96, 3, 8, 1, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("pf rows96 nb3 8w pfk1 a4", [&] { k_dma_pf<96, 3, 8, 1, 4><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("pf rows96 nb3 8w pfk2 a2", [&] { k_dma_pf<96, 3, 8, 2, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("pf rows96 nb3 8w pfk4 a1", [&] { k_dma_pf<96, 3, 8, 4, 1><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("pf rows96 nb3 8w pfk4 a2", [&] { k_dma_pf<96, 3, 8, 4, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("pf rows96 nb2 8w pfk2 a2", [&] { k_dma_pf<96, 2, 8, 2, 2><<<ncu, 512>>>(d, S, nreg, len, o); });
-  timeit("pf rows192 nb2 6w pfk2 a2", [&] { k_dma_pf<192, 2, 6, 2, 2><<<ncu, 384>>>(d, S, nreg, len, o); });
-  for (uint32_t S2 : {1056u, 2064u, 4128u}) {
-    const uint32_t nr2 = (uint32_t)((len + 64ull * S2 - 1) / (64ull * S2)) - 1;
-    char nm[64];
-    snprintf(nm, sizeof nm, "dma rows96 nb3 8w S=%u", S2);
-    timeit(nm, [&] { k_dma<96, 3, 8><<<ncu, 512>>>(d, S2, nr2, len, o); });
-    snprintf(nm, sizeof nm, "pf rows96 nb3 8w pfk1 a2 S=%u", S2);
-    timeit(nm, [&] { k_dma_pf<96, 3, 8, 1, 2><<<ncu, 512>>>(d, S2, nr2, len, o); });
+  for (uint32_t S : {8448u, 33024u, 2304u}) {
+    const uint32_t nreg = (uint32_t)(len / (64ull * S));
+    char nm[96];
+#define RUN(ROWB, NB, W, label) snprintf(nm, sizeof nm, "S=%u " label, S); \
+    timeit(nm, [&] { k_dma<ROWB, NB, W><<<ncu, W * 64>>>(d, S, nreg, len, o); });
+    RUN(128, 2, 8, "rows128 1-ahead 8w")
+    RUN(128, 3, 6, "rows128 2-ahead 6w")
+    RUN(128, 4, 4, "rows128 3-ahead 4w")
+    RUN(256, 2, 4, "rows256 1-ahead 4w")
+    RUN(128, 1, 16, "rows128 0-ahead 16w")
+    RUN(64, 2, 16, "rows64 1-ahead 16w")
+    RUN(96, 3, 8, "rows96 2-ahead 8w (old)")
+#undef RUN
+#define RUNPF(ROWB, NB, W, PFK, AH, label) snprintf(nm, sizeof nm, "S=%u " label, S); \
+    timeit(nm, [&] { k_dma_pf<ROWB, NB, W, PFK, AH><<<ncu, W * 64>>>(d, S, nreg, len, o); });
+    RUNPF(128, 2, 8, 1, 1, "pf rows128 1-ahead 8w pfk1 a1")
+    RUNPF(128, 2, 8, 1, 2, "pf rows128 1-ahead 8w pfk1 a2")
+    RUNPF(128, 2, 8, 2, 1, "pf rows128 1-ahead 8w pfk2 a1")
+    RUNPF(128, 2, 8, 4, 1, "pf rows128 1-ahead 8w pfk4 a1")
+#undef RUNPF
   }
   return 0;
 }
