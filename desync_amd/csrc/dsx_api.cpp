@@ -107,9 +107,11 @@ struct dsx_ctx {
   int regions_per_slot = 1;           // DSX_REGIONS_PER_SLOT: scan work units per wave slot
   int scan_cfg = 0;                   // DSX_SCAN_CFG: index into kCfg* (waves, rounds/batch, LDS buffers)
   bool scan_line = true;              // DSX_SCAN_LINE=0: 96-B-row scan_kernel instead of scanl_kernel
-  int scanl_waves = 8;                // DSX_SCANL_WAVES: 8 or 12
-  int scanl_sub = 8;                  // DSX_SCANL_SUB: 4 or 8 (12-wave kernel)
+  int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
+  bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
+  DevBuf<uint64_t> trace;
+  uint64_t trace_n = 0;
   uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
@@ -324,8 +326,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
-  if (const char* v = getenv("DSX_SCANL_WAVES")) c->scanl_waves = atoi(v) == 12 ? 12 : 8;
-  if (const char* v = getenv("DSX_SCANL_SUB")) c->scanl_sub = atoi(v) == 4 ? 4 : 8;
+  if (const char* v = getenv("DSX_SCAN_TRACE")) c->scan_trace = atoi(v) != 0;
   if (const char* v = getenv("DSX_LANE_TARGET"))
     c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
@@ -382,6 +383,17 @@ extern "C" const char* dsx_last_error(dsx_ctx_t* c) { return c ? c->err.c_str() 
 extern "C" int dsx_cancel(dsx_ctx_t* c) {
   if (!c) return DSX_E_INVAL;
   c->cancel.store(1);
+  return DSX_OK;
+}
+
+extern "C" int dsx_debug_scan_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64_t* n) {
+  if (!c || !n) return DSX_E_INVAL;
+  *n = c->trace_n;
+  if (!c->trace_n || !out) return DSX_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t k = std::min<uint64_t>(cap, 3 * c->trace_n);
+  HIPCHK(c, hipMemcpy(out, c->trace.p, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return DSX_OK;
 }
 
@@ -535,6 +547,12 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
                     : (uint32_t)(16 * (((uint64_t)kLine + delta - hmin) / 16));
   }
   c->last_grid_P = line ? P - delta : P;
+  if (c->scan_trace && line) {
+    c->trace_n = (uint64_t)c->ncu * W;
+    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n));
+    HIPCHK(c, hipMemsetAsync(c->trace.p, 0, 3 * c->trace_n * sizeof(uint64_t), c->stream));
+    sa.trace = c->trace.p;
+  }
   c->init_pending = false;
   const uint32_t pi = c->npiece_call++;
   while (c->pev.size() < 3 * (size_t)(pi + 1)) {
@@ -579,9 +597,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
       hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB>), g, b, 0, c->stream, sa);          \
   } while (0)
     if (line) {
-      if (W == 12 && c->scanl_sub == 4) DSX_LAUNCHL(12, 4);
-      else if (W == 12) DSX_LAUNCHL(12, 8);
-      else DSX_LAUNCHL(8, 8);
+      DSX_LAUNCHL(8, 8);
     } else switch (c->scan_cfg) {
       case 1: DSX_LAUNCH(1, 2, 12, 4, false); break;
       case 2: DSX_LAUNCH(1, 2, 16, 4, false); break;

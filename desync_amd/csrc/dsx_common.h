@@ -70,6 +70,7 @@ struct ScanArgs {
   // into its warm-up line (bytes before it read as zeros)
   uint32_t delta;
   uint32_t shift0;
+  uint64_t* trace;       // diagnostics (DSX_SCAN_TRACE): per wave slot {start, end, regions}
 };
 
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches

@@ -541,8 +541,9 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   constexpr int STG = kWave * kLine;         // staging bytes per wave
   constexpr int LDSB = kTableBytes + W * STG;
   constexpr int NT = W * kWave;
-  static_assert(LDSB <= kScanLds, "LDS budget");
+  static_assert(LDSB + 4 * W <= kScanLds, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
+  __shared__ uint32_t s_prog[W];  // batches hashed per wave (SIMD partner balancing)
 
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *a.overflow_next = 0u;
@@ -561,19 +562,35 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     for (int e = threadIdx.x; e < W * STG / 4; e += NT)
       reinterpret_cast<uint32_t*>(lds + kTableBytes)[e] = 0u;
   }
-  for (int e = threadIdx.x; e < 256 * 32; e += NT) {
-    const uint32_t v = kT[e >> 5];
+  // one table load per thread (a loop of dependent loads cost ~15 us of the
+  // launch): thread t writes byte value t % 256 into slots of its share
+  {
+    static_assert(NT % 256 == 0 && 32 % (NT / 256) == 0, "table fill shape");
+    constexpr int SPT = 32 / (NT / 256);  // slots per thread
+    const uint32_t v = threadIdx.x & 255u;
+    const uint32_t tv = kT[v];
     uint2 t;
-    t.x = v;
-    t.y = __builtin_amdgcn_alignbit(v, v, 16);
-    *reinterpret_cast<uint2*>(lds + (e >> 5) * 256 + (e & 31) * 8) = t;
+    t.x = tv;
+    t.y = __builtin_amdgcn_alignbit(tv, tv, 16);
+    const uint32_t s0 = (threadIdx.x >> 8) * SPT;
+#pragma unroll
+    for (int k = 0; k < SPT; ++k)
+      *reinterpret_cast<uint2*>(lds + v * 256u + (s0 + k) * 8u) = t;
   }
+  if (threadIdx.x < W) s_prog[threadIdx.x] = 0u;
   __syncthreads();
 
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t slot8 = (lane & 31u) * 8u;
   uint8_t* stage = lds + kTableBytes + wave * STG;
+  // Waves w and w + W/2 share a SIMD (waves are placed on the SIMDs
+  // cyclically).  VALU issue favours the older wave, so left alone the
+  // younger one finishes ~25 % later and the SIMD ends the scan with one wave
+  // (tools/scan_trace.py).  Each batch, the wave that has hashed fewer
+  // batches than its partner takes issue priority.
+  const uint32_t partner = (wave + (uint32_t)W / 2u) % (uint32_t)W;
+  uint32_t my_prog = 0;
   const uint32_t stage_lds =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)stage);
   const uint32_t S = a.lane_bytes;
@@ -627,6 +644,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 
   uint32_t region = blockIdx.x * W + wave;
   if (region >= a.nregions) return;
+  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint32_t nreg_done = 0;
   u32x4 rsrc;
   uint32_t sh;
   desc_of(region, rsrc, sh);
@@ -656,6 +675,9 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     // wait for batch b, copy this lane's row to registers, issue batch b+1
     // (or the next region's warm-up line) into the freed staging line
     auto fetch = [&](uint32_t b) {
+      ++my_prog;
+      s_prog[wave] = my_prog;
+      const uint32_t their = s_prog[partner];
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint8_t* my_row = stage + lane * (uint32_t)kLine;
 #pragma unroll
@@ -668,6 +690,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         w[4 * c + 3] = q.w;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (__builtin_amdgcn_readfirstlane(their) < my_prog)
+        __builtin_amdgcn_s_setprio(0);
+      else
+        __builtin_amdgcn_s_setprio(1);
       if (b + 1u < NB)
         issue(rsrc, sh, b + 1u);
       else
@@ -741,12 +767,19 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       a.region_cnt[region] = exact;
       if (lane_ovf || exact > a.region_cap) atomicAdd(a.overflow, 1u);
     }
+    ++nreg_done;
     if (next >= a.nregions) break;
     region = next;
     rsrc = nrsrc;
     sh = nsh;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.trace && lane == 0) {
+    uint64_t* tr = a.trace + 3ull * (blockIdx.x * W + wave);
+    tr[0] = t_start;
+    tr[1] = __builtin_amdgcn_s_memrealtime();
+    tr[2] = nreg_done;
+  }
 }
 
 #define DSX_SCANL_INST(W, SUB)                                         \
@@ -757,8 +790,6 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   template __global__ void scanl_kernel<2, 3, W, SUB>(ScanArgs);       \
   template __global__ void scanl_kernel<2, 4, W, SUB>(ScanArgs);
 DSX_SCANL_INST(8, 8)
-DSX_SCANL_INST(12, 8)
-DSX_SCANL_INST(12, 4)
 
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1
 // (the plain form of chunker_test.go:190-213).  Diagnostic entry point.

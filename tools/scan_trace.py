@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the line-aligned scan (DSX_SCAN_TRACE=1): start/end
+spread over the wave slots, by wave index within the workgroup, for one
+device-resident blob (uniform, default params)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+os.environ["DSX_SCAN_TRACE"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import desync_amd  # noqa: E402
+from desync_amd import _lib  # noqa: E402
+
+gib = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
+W = int(os.environ.get("DSX_SCANL_WAVES", "8"))
+n = int(gib * (1 << 30))
+ctx = _lib.Context(0)
+L = _lib.lib()
+t = torch.empty(n, dtype=torch.uint8, device="cuda")
+_lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 1), ctx.h)
+for _ in range(3):
+    desync_amd.cut_device(t.data_ptr(), n, 16384, 65536, 262144, ctx=ctx)
+cnt = ctypes.c_uint64()
+_lib.check(L.dsx_debug_scan_trace(ctx.h, None, 0, ctypes.byref(cnt)), ctx.h)
+buf = np.zeros(3 * cnt.value, np.uint64)
+_lib.check(L.dsx_debug_scan_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(cnt)), ctx.h)
+tr = buf.reshape(-1, 3).astype(np.int64)
+tr = tr[tr[:, 1] > 0]
+t0 = tr[:, 0].min()
+st = (tr[:, 0] - t0) / 100.0  # us (100 MHz)
+en = (tr[:, 1] - t0) / 100.0
+print(f"waves {len(tr)}  regions/wave {np.bincount(tr[:, 2].astype(int)).tolist()}")
+q = [0, 1, 10, 50, 90, 99, 100]
+print("start us  pct", q, np.percentile(st, q).round(1).tolist())
+print("end   us  pct", q, np.percentile(en, q).round(1).tolist())
+wi = np.arange(len(tr)) % W
+for w in range(W):
+    print(f"  wave {w}: end median {np.median(en[wi == w]):7.1f}  max {en[wi == w].max():7.1f}")
