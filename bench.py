@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--workload", default="uniform", choices=["uniform", "dedup", "zeros"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="N=1: chunking jobs kept in flight (one library context each), so "
+                         "the host's wait for job k overlaps the GPU work of job k+1")
     ap.add_argument("--check", action="store_true",
                     help="N>1: compare the concatenated per-rank cut lists with one "
                          "dsx_cut_device over the whole blob on rank 0 (small sizes)")
@@ -148,34 +151,64 @@ def main():
         from desync_amd.shard import DeviceShard
         shard = DeviceShard(ctx, d_ptr, halo, rank * n, n, n * world, p)
 
-    def step():
+    # N = 1: every step is one complete dsx_cut_device job (scan + stitch, cut
+    # list in HBM) whose count the host collects.  Jobs rotate over `inflight`
+    # contexts (own stream and scratch each): job s is enqueued before the
+    # host waits for job s-1, so the GPU is not idle while the host wakes up.
+    nctx = max(1, args.inflight) if world == 1 else 1
+    ctxs = [ctx] + [_lib.Context(gpu) for _ in range(nctx - 1)]
+    outs = [out] + [torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(nctx - 1)]
+    pending = [False] * nctx
+    scan_ms = []
+    stitch_ms = []
+    cnt = ctypes.c_uint64()
+
+    def collect(i, record):
+        c = ctxs[i]
+        _lib.check(L.dsx_result(c.h, ctypes.byref(cnt)), c.h)
+        pending[i] = False
+        if record:
+            st = c.stats()
+            scan_ms.append(st.scan_ms)
+            stitch_ms.append(st.stitch_ms)
+        return cnt.value
+
+    def step(s, record=False):
         if world == 1:
-            _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
-                                        ctypes.c_void_p(out.data_ptr()), cap,
+            i = s % nctx
+            got = collect(i, record) if pending[i] else None
+            c = ctxs[i]
+            _lib.check(L.dsx_cut_device(c.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
+                                        ctypes.c_void_p(outs[i].data_ptr()), cap,
                                         ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
-                       ctx.h)
-            _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
-            return cnt.value
+                       c.h)
+            pending[i] = True
+            return got
         # N > 1: chunk this rank's shard, RCCL all-gather of the 16 KiB seam
         # records in HBM, resolve the seams (desync_amd/shard.py)
         return shard.run()
 
-    cnt = ctypes.c_uint64()
-    for _ in range(args.warmup):
-        step()
+    def drain(nsteps, record):
+        last = None
+        for j in range(nctx):
+            i = (nsteps + j) % nctx  # oldest job first
+            if pending[i]:
+                last = collect(i, record)
+        return last
+
+    for s in range(args.warmup):
+        step(s)
+    drain(args.warmup, False)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    scan_ms = []
-    stitch_ms = []
     t0 = time.perf_counter()
     chunks = 0
-    for _ in range(args.steps):
-        chunks = step()
-        if world == 1:
-            st = ctx.stats()
-            scan_ms.append(st.scan_ms)
-            stitch_ms.append(st.stitch_ms)
+    for s in range(args.steps):
+        r = step(s, record=True)
+        chunks = r if r is not None else chunks
+    if world == 1:
+        chunks = drain(args.steps, True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -190,6 +223,21 @@ def main():
         chunks = int(tc.item())
     ms_per_step = dt / args.steps * 1000.0
     value = (n * world * args.steps) / dt / GiB
+
+    # roofline timing: with jobs in flight a scan's HIP events also bracket
+    # the other contexts' kernels, so the per-launch scan duration comes from
+    # a serial pass (one job at a time, same inputs) right after the timed loop
+    if world == 1:
+        scan_ms.clear()
+        stitch_ms.clear()
+        for _ in range(args.steps):
+            _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
+                                        ctypes.c_void_p(out.data_ptr()), cap,
+                                        ctypes.byref(cnt), _lib.DSX_OUT_DEVICE), ctx.h)
+            assert cnt.value == chunks, "serial pass disagrees with the timed jobs"
+            st = ctx.stats()
+            scan_ms.append(st.scan_ms)
+            stitch_ms.append(st.stitch_ms)
 
     if args.check and world > 1:
         mine = torch.from_numpy(shard.cuts().astype(np.int64))
@@ -222,6 +270,7 @@ def main():
                 "bytes_per_gpu": n,
                 "chunks": int(chunks),
                 "parallelism": f"range-shard x{world}" if world > 1 else "single GPU",
+                "jobs_in_flight": nctx,
             },
         }
         if world == 1 and scan_ms:
@@ -235,7 +284,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "dsx::scan_kernel",
+                "kernel": "dsx::scanl_kernel",
                 "kernel_ms": round(avg_scan, 4),
                 "stitch_ms": round(float(np.mean(stitch_ms)), 4),
             }
@@ -245,7 +294,8 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
-    ctx.close()
+    for c in ctxs:
+        c.close()
 
 
 if __name__ == "__main__":

@@ -47,7 +47,7 @@ EXPORTS = (
     "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
     "dsx_stream_done", "dsx_stream_chunk_data", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
-    "dsx_get_stats", "dsx_debug_scan_trace",
+    "dsx_get_stats", "dsx_debug_trace",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -144,7 +144,7 @@ def lib():
             "dsx_gen_dedup": (i32, [vp, vp, u64, u64, u64, ctypes.c_double]),
             "dsx_chunk_ids": (i32, [vp, vp, u64, u64, vp, u64, vp, u32, i32]),
             "dsx_get_stats": (i32, [vp, P(Stats)]),
-            "dsx_debug_scan_trace": (i32, [vp, vp, u64, P(u64)]),
+            "dsx_debug_trace": (i32, [vp, vp, u64, P(u64), P(u64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

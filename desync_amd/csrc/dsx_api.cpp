@@ -110,8 +110,8 @@ struct dsx_ctx {
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
-  DevBuf<uint64_t> trace;
-  uint64_t trace_n = 0;
+  DevBuf<uint64_t> trace;       // [3 * trace_n scan records][5 * trace_walk_n walk records]
+  uint64_t trace_n = 0, trace_walk_n = 0;
   uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
@@ -386,13 +386,16 @@ extern "C" int dsx_cancel(dsx_ctx_t* c) {
   return DSX_OK;
 }
 
-extern "C" int dsx_debug_scan_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64_t* n) {
-  if (!c || !n) return DSX_E_INVAL;
-  *n = c->trace_n;
-  if (!c->trace_n || !out) return DSX_OK;
+extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64_t* n_scan,
+                               uint64_t* n_walk) {
+  if (!c || !n_scan || !n_walk) return DSX_E_INVAL;
+  *n_scan = c->trace_n;
+  *n_walk = c->trace_walk_n;
+  const uint64_t words = 3 * c->trace_n + 5 * c->trace_walk_n;
+  if (!words || !out) return DSX_OK;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint64_t k = std::min<uint64_t>(cap, 3 * c->trace_n);
+  const uint64_t k = std::min<uint64_t>(cap, words);
   HIPCHK(c, hipMemcpy(out, c->trace.p, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return DSX_OK;
 }
@@ -549,7 +552,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   c->last_grid_P = line ? P - delta : P;
   if (c->scan_trace && line) {
     c->trace_n = (uint64_t)c->ncu * W;
-    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n));
+    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n + 5 * 65536));
     HIPCHK(c, hipMemsetAsync(c->trace.p, 0, 3 * c->trace_n * sizeof(uint64_t), c->stream));
     sa.trace = c->trace.p;
   }
@@ -666,6 +669,10 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.host_state = c->h_state;
   ta.seq = seq;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
+  if (c->scan_trace && line && walk_grid <= 65536) {
+    ta.trace = c->trace.p + 3 * c->trace_n;
+    c->trace_walk_n = walk_grid;
+  }
   const size_t walk_lds = (size_t)kWalkLdsCap * 4 + (kMaxSpg + 1) * 8;
   hipLaunchKernelGGL(walk_kernel, dim3(walk_grid), dim3(256), walk_lds, c->stream, ta);
   HIPCHK(c, hipGetLastError());

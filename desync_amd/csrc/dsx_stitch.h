@@ -84,6 +84,7 @@ struct StitchArgs {
   DevState* state;
   HostState* host_state;  // pinned, written by fixup_kernel (may be null)
   uint64_t seq;
+  uint64_t* trace;        // diagnostics: per walk workgroup 5 timestamps (may be null)
 };
 
 }  // namespace dsx

@@ -61,6 +61,43 @@ struct LdsSrc {
   }
 };
 
+// The same source searched by a whole wavefront: 64 candidates per LDS read
+// and a ballot, so a chain step costs one LDS round trip instead of one per
+// candidate passed (the walks are latency-bound: one chain per wave).
+struct WaveLdsSrc {
+  const uint32_t* c;
+  uint32_t n;
+  uint32_t j;
+  uint64_t lo;
+  uint32_t lane;
+  // j <- first index with c[j] > ar (or n)
+  __device__ void advance(uint64_t ar) {
+    while (j < n) {
+      const uint32_t idx = j + lane;
+      const uint32_t v = idx < n ? c[idx] : 0xFFFFFFFFu;
+      const uint64_t m = __ballot((uint64_t)v > ar || idx >= n);
+      if (m) {
+        j += (uint32_t)__builtin_ctzll(m);
+        if (j > n) j = n;
+        return;
+      }
+      j += 64;
+    }
+  }
+  __device__ uint64_t first_in(uint64_t a, uint64_t b) {
+    advance(a - lo);  // a >= lo always (a = s+min, s >= lo)
+    if (j < n) {
+      const uint64_t p = lo + c[j];
+      if (p <= b) return p;
+    }
+    return kNone;
+  }
+  __device__ void seek(uint64_t a) {
+    j = 0;
+    advance(a < lo ? 0 : a - lo);
+  }
+};
+
 // Candidates straight from the scan's per-region sorted lists (global
 // memory); used by the sequential repair only.
 struct GlobalSrc {
@@ -149,6 +186,8 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   __shared__ uint32_t s_off[kWalkMaxRegions + 1];
   __shared__ uint32_t s_wave[kWalkThreads / 64];
 
+  uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 5ull * blockIdx.x : nullptr;
+  if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
   const DevState* st = a.state;
   if (st->done || *a.pc.overflow) return;  // finished, or scan lists overflowed
   const uint64_t s0 = st->carry;
@@ -185,6 +224,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     __syncthreads();
     dense = total > a.lds_cap;
   }
+  if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
   if (!dense) {
     // one candidate per thread: find its region by binary search over s_off
     for (uint32_t g = threadIdx.x; g < total; g += kWalkThreads) {
@@ -200,66 +240,82 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     }
   }
   __syncthreads();
+  if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
 
   const uint32_t nwalk = kB - kFirst + 1;
-  // ---- phase 1: speculative chain of each segment -> exit X_k ----
-  if (!dense && threadIdx.x < nwalk) {
-    const uint32_t k = kFirst + threadIdx.x;
-    const uint64_t v = seg_start(a, s0, k);
-    const uint64_t e = seg_end(a, k);
-    LdsSrc src{cand, total, 0, lo};
-    src.seek(v);
-    uint64_t x = v, last = v;
-    while (true) {
-      if (a.chain.is_last && x >= a.chain.L) break;
-      const uint64_t nx = next_cut(x, src, a.chain);
-      if (nx == kUndet || nx > e) break;
-      last = nx;
-      x = nx;
-    }
-    xs[threadIdx.x] = last;
-    if (k >= kA) a.seg_info[k].X = last;  // kA-1 belongs to the previous workgroup
-  }
-  __syncthreads();
-
-  // ---- phase 2: staged chain entering from X_{k-1} ----
-  const uint32_t t = threadIdx.x + (kA - kFirst);
-  if (threadIdx.x < kB - kA + 1) {
-    const uint32_t k = kA + threadIdx.x;
-    SegInfo& si = a.seg_info[k];
-    if (dense) {
-      si.E = kUndet;
-      si.Z = kUndet;
-      si.X = kUndet;  // forces the repair of this and the next segment
-      si.cnt = 0;
-      si.flags = kSegDense;
-    } else {
-      const uint64_t E = (k == 0) ? s0 : xs[t - 1];
-      const uint64_t sst = seg_start(a, s0, k);
+  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  constexpr uint32_t kWaves = kWalkThreads / 64;
+  // ---- phase 1: speculative chain of each segment -> exit X_k (one wave each) ----
+  if (!dense) {
+    for (uint32_t t = wv; t < nwalk; t += kWaves) {
+      const uint32_t k = kFirst + t;
+      const uint64_t v = seg_start(a, s0, k);
       const uint64_t e = seg_end(a, k);
-      LdsSrc src{cand, total, 0, lo};
-      src.seek(E);
-      uint64_t* out = a.stage + (uint64_t)k * a.scap;
-      uint32_t n = 0, flags = 0;
-      uint64_t x = E, last = E;
+      WaveLdsSrc src{cand, total, 0, lo, ln};
+      src.seek(v);
+      uint64_t x = v, last = v;
       while (true) {
-        if (a.chain.is_last && x >= a.chain.L) { flags |= kSegEnd; break; }
+        if (a.chain.is_last && x >= a.chain.L) break;
         const uint64_t nx = next_cut(x, src, a.chain);
-        if (nx == kUndet) { flags |= kSegUndet; break; }
-        if (nx > e) break;
-        if (nx > sst) {
-          if (n < a.scap) out[n] = nx;
-          ++n;
-        }
+        if (nx == kUndet || nx > e) break;
         last = nx;
         x = nx;
       }
-      if (n > a.scap) flags |= kSegOverflow;
+      if (ln == 0) {
+        xs[t] = last;
+        if (k >= kA) a.seg_info[k].X = last;  // kA-1 belongs to the previous workgroup
+      }
+    }
+  }
+  __syncthreads();
+  if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+
+  // ---- phase 2: staged chain entering from X_{k-1} (one wave each) ----
+  for (uint32_t i = wv; i < kB - kA + 1; i += kWaves) {
+    const uint32_t k = kA + i;
+    const uint32_t t = i + (kA - kFirst);
+    SegInfo& si = a.seg_info[k];
+    if (dense) {
+      if (ln == 0) {
+        si.E = kUndet;
+        si.Z = kUndet;
+        si.X = kUndet;  // forces the repair of this and the next segment
+        si.cnt = 0;
+        si.flags = kSegDense;
+      }
+      continue;
+    }
+    const uint64_t E = (k == 0) ? s0 : xs[t - 1];
+    const uint64_t sst = seg_start(a, s0, k);
+    const uint64_t e = seg_end(a, k);
+    WaveLdsSrc src{cand, total, 0, lo, ln};
+    src.seek(E);
+    uint64_t* out = a.stage + (uint64_t)k * a.scap;
+    uint32_t n = 0, flags = 0;
+    uint64_t x = E, last = E;
+    while (true) {
+      if (a.chain.is_last && x >= a.chain.L) { flags |= kSegEnd; break; }
+      const uint64_t nx = next_cut(x, src, a.chain);
+      if (nx == kUndet) { flags |= kSegUndet; break; }
+      if (nx > e) break;
+      if (nx > sst) {
+        if (ln == (n & 63u) && n < a.scap) out[n] = nx;  // spread the stores over lanes
+        ++n;
+      }
+      last = nx;
+      x = nx;
+    }
+    if (n > a.scap) flags |= kSegOverflow;
+    if (ln == 0) {
       si.E = E;
       si.Z = last;
       si.cnt = n;
       si.flags = flags;
     }
+  }
+  if (a.trace) {
+    __syncthreads();
+    if (tr) tr[4] = __builtin_amdgcn_s_memrealtime();
   }
 }
 

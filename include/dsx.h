@@ -195,10 +195,14 @@ int dsx_shard_resolve(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, int ran
 int dsx_selftest_boundary(dsx_ctx_t *ctx, const dsx_params_t *p, int mode, uint64_t h0,
                           uint64_t n, uint64_t *mismatches);
 
-/* Per-wave-slot records {start, end, regions} of the last line-aligned scan
- * (s_memrealtime ticks, 100 MHz) when the context was created with
- * DSX_SCAN_TRACE=1; *n = wave slots.  Copies min(cap, 3*n) words to out. */
-int dsx_debug_scan_trace(dsx_ctx_t *ctx, uint64_t *out, uint64_t cap, uint64_t *n);
+/* Timeline of the last piece when the context was created with
+ * DSX_SCAN_TRACE=1 (s_memrealtime ticks, 100 MHz): *n_scan wave-slot records
+ * {start, end, regions} of the line-aligned scan, then *n_walk stitch-walk
+ * workgroup records {entry, counts scanned, candidates staged, speculative
+ * walks done, staged walks done}.  Copies min(cap, 3*n_scan + 5*n_walk)
+ * words to out. */
+int dsx_debug_trace(dsx_ctx_t *ctx, uint64_t *out, uint64_t cap, uint64_t *n_scan,
+                    uint64_t *n_walk);
 
 /* ---- synthetic inputs (bench / tests; generated on device) ------------------ */
 /* bytes [offset, offset+len) of the seeded uniform stream (splitmix64 of the

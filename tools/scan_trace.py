@@ -23,11 +23,13 @@ t = torch.empty(n, dtype=torch.uint8, device="cuda")
 _lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 1), ctx.h)
 for _ in range(3):
     desync_amd.cut_device(t.data_ptr(), n, 16384, 65536, 262144, ctx=ctx)
-cnt = ctypes.c_uint64()
-_lib.check(L.dsx_debug_scan_trace(ctx.h, None, 0, ctypes.byref(cnt)), ctx.h)
-buf = np.zeros(3 * cnt.value, np.uint64)
-_lib.check(L.dsx_debug_scan_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(cnt)), ctx.h)
-tr = buf.reshape(-1, 3).astype(np.int64)
+ns, nw = ctypes.c_uint64(), ctypes.c_uint64()
+_lib.check(L.dsx_debug_trace(ctx.h, None, 0, ctypes.byref(ns), ctypes.byref(nw)), ctx.h)
+buf = np.zeros(3 * ns.value + 5 * nw.value, np.uint64)
+_lib.check(L.dsx_debug_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(ns),
+                             ctypes.byref(nw)), ctx.h)
+tr = buf[:3 * ns.value].reshape(-1, 3).astype(np.int64)
+wk = buf[3 * ns.value:].reshape(-1, 5).astype(np.int64)
 tr = tr[tr[:, 1] > 0]
 t0 = tr[:, 0].min()
 st = (tr[:, 0] - t0) / 100.0  # us (100 MHz)
@@ -39,3 +41,9 @@ print("end   us  pct", q, np.percentile(en, q).round(1).tolist())
 wi = np.arange(len(tr)) % W
 for w in range(W):
     print(f"  wave {w}: end median {np.median(en[wi == w]):7.1f}  max {en[wi == w].max():7.1f}")
+wk = wk[wk[:, 4] > 0]
+if len(wk):
+    rel = (wk - t0) / 100.0
+    print(f"walk workgroups {len(wk)} (times from the first scan wave start, us)")
+    for i, name in enumerate(["entry", "counts", "staged", "walk1", "walk2"]):
+        print(f"  {name:7s} pct {q} {np.percentile(rel[:, i], q).round(1).tolist()}")
