@@ -110,7 +110,7 @@ struct dsx_ctx {
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
-  DevBuf<uint64_t> trace;       // [3 * trace_n scan records][5 * trace_walk_n walk records]
+  DevBuf<uint64_t> trace;       // [3 * trace_n scan records][7 * trace_walk_n walk records]
   uint64_t trace_n = 0, trace_walk_n = 0;
   uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
 
@@ -391,7 +391,7 @@ extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64
   if (!c || !n_scan || !n_walk) return DSX_E_INVAL;
   *n_scan = c->trace_n;
   *n_walk = c->trace_walk_n;
-  const uint64_t words = 3 * c->trace_n + 5 * c->trace_walk_n;
+  const uint64_t words = 3 * c->trace_n + 7 * c->trace_walk_n;
   if (!words || !out) return DSX_OK;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -552,7 +552,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   c->last_grid_P = line ? P - delta : P;
   if (c->scan_trace && line) {
     c->trace_n = (uint64_t)c->ncu * W;
-    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n + 5 * 65536));
+    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n + 7 * 65536));
     HIPCHK(c, hipMemsetAsync(c->trace.p, 0, 3 * c->trace_n * sizeof(uint64_t), c->stream));
     sa.trace = c->trace.p;
   }

@@ -98,6 +98,13 @@ struct WaveLdsSrc {
   }
 };
 
+// wave-uniform 64-bit value (scalar registers, scalar control flow)
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Candidates straight from the scan's per-region sorted lists (global
 // memory); used by the sequential repair only.
 struct GlobalSrc {
@@ -186,7 +193,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   __shared__ uint32_t s_off[kWalkMaxRegions + 1];
   __shared__ uint32_t s_wave[kWalkThreads / 64];
 
-  uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 5ull * blockIdx.x : nullptr;
+  uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 7ull * blockIdx.x : nullptr;
   if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
   const DevState* st = a.state;
   if (st->done || *a.pc.overflow) return;  // finished, or scan lists overflowed
@@ -240,7 +247,10 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     }
   }
   __syncthreads();
-  if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
+  if (tr) {
+    tr[2] = __builtin_amdgcn_s_memrealtime();
+    tr[5] = __builtin_amdgcn_s_memtime();
+  }
 
   const uint32_t nwalk = kB - kFirst + 1;
   const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -268,7 +278,10 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     }
   }
   __syncthreads();
-  if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+  if (tr) {
+    tr[3] = __builtin_amdgcn_s_memrealtime();
+    tr[6] = __builtin_amdgcn_s_memtime();
+  }
 
   // ---- phase 2: staged chain entering from X_{k-1} (one wave each) ----
   for (uint32_t i = wv; i < kB - kA + 1; i += kWaves) {

@@ -199,8 +199,9 @@ int dsx_selftest_boundary(dsx_ctx_t *ctx, const dsx_params_t *p, int mode, uint6
  * DSX_SCAN_TRACE=1 (s_memrealtime ticks, 100 MHz): *n_scan wave-slot records
  * {start, end, regions} of the line-aligned scan, then *n_walk stitch-walk
  * workgroup records {entry, counts scanned, candidates staged, speculative
- * walks done, staged walks done}.  Copies min(cap, 3*n_scan + 5*n_walk)
- * words to out. */
+ * walks done, staged walks done, s_memtime at staged, s_memtime at
+ * speculative walks done}.  Copies min(cap, 3*n_scan + 7*n_walk) words to
+ * out. */
 int dsx_debug_trace(dsx_ctx_t *ctx, uint64_t *out, uint64_t cap, uint64_t *n_scan,
                     uint64_t *n_walk);
 

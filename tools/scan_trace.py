@@ -9,6 +9,7 @@ import sys
 import numpy as np
 
 os.environ["DSX_SCAN_TRACE"] = "1"
+print("scan_trace: importing torch", flush=True)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import desync_amd  # noqa: E402
@@ -21,15 +22,16 @@ ctx = _lib.Context(0)
 L = _lib.lib()
 t = torch.empty(n, dtype=torch.uint8, device="cuda")
 _lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 1), ctx.h)
-for _ in range(3):
+for i in range(3):
+    print(f"scan_trace: call {i}", flush=True)
     desync_amd.cut_device(t.data_ptr(), n, 16384, 65536, 262144, ctx=ctx)
 ns, nw = ctypes.c_uint64(), ctypes.c_uint64()
 _lib.check(L.dsx_debug_trace(ctx.h, None, 0, ctypes.byref(ns), ctypes.byref(nw)), ctx.h)
-buf = np.zeros(3 * ns.value + 5 * nw.value, np.uint64)
+buf = np.zeros(3 * ns.value + 7 * nw.value, np.uint64)
 _lib.check(L.dsx_debug_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(ns),
                              ctypes.byref(nw)), ctx.h)
 tr = buf[:3 * ns.value].reshape(-1, 3).astype(np.int64)
-wk = buf[3 * ns.value:].reshape(-1, 5).astype(np.int64)
+wk = buf[3 * ns.value:].reshape(-1, 7).astype(np.int64)
 tr = tr[tr[:, 1] > 0]
 t0 = tr[:, 0].min()
 st = (tr[:, 0] - t0) / 100.0  # us (100 MHz)
@@ -43,7 +45,9 @@ for w in range(W):
     print(f"  wave {w}: end median {np.median(en[wi == w]):7.1f}  max {en[wi == w].max():7.1f}")
 wk = wk[wk[:, 4] > 0]
 if len(wk):
-    rel = (wk - t0) / 100.0
+    rel = (wk[:, :5] - t0) / 100.0
+    cyc = (wk[:, 6] - wk[:, 5]) / np.maximum(1, wk[:, 3] - wk[:, 2]) * 100.0
+    print(f"walk phase 1 shader clock MHz median {np.median(cyc):.0f}")
     print(f"walk workgroups {len(wk)} (times from the first scan wave start, us)")
     for i, name in enumerate(["entry", "counts", "staged", "walk1", "walk2"]):
         print(f"  {name:7s} pct {q} {np.percentile(rel[:, i], q).round(1).tolist()}")
