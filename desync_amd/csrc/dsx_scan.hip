@@ -30,11 +30,22 @@
 
 #include "../../include/dsx_buzhash_table.h"
 #include <type_traits>
+#include <utility>
 #include "dsx_common.h"
 
 namespace dsx {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+
+// f(integral_constant<int, G>) for G = 0..N-1, unrolled at compile time
+template <class F, int... G>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, G...>) {
+  (f(std::integral_constant<int, G>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __constant__ uint32_t kT[256] = DSX_BUZHASH_TABLE_INIT;
@@ -101,7 +112,11 @@ __device__ __forceinline__ uint32_t mode2_t_mad(uint32_t h, uint32_t inv_v, uint
 }
 __device__ __forceinline__ bool mode2_exact(uint32_t t, const TestConsts& tc) {
   const uint32_t h = (t - tc.tadd) * tc.dodd;  // inv * dodd == 1 (mod 2^32)
-  return t < tc.vmax && h % tc.d == tc.dm1;
+  // chunker.go:265's multiply-inverse form (no division: a `%` here costs a
+  // magic-number register that spills on the rare path of the scan)
+  uint32_t v = (h + 1u) * tc.inv;
+  v = __builtin_amdgcn_alignbit(v, v, tc.rot);
+  return t < tc.vmax && v - tc.qbias <= tc.qmax;
 }
 
 template <int MODE>
@@ -603,14 +618,12 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // chunk c at physical (c + rot(r)) % 8 with rot(r) = (r >> 1) % 8, which
   // makes the ds_read_b128 row reads conflict-free (each 16-lane group covers
   // the 16 distinct {row parity, chunk} bank quads).
-  uint32_t dma_off[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const uint32_t u = (uint32_t)i * 64u + lane;
-    const uint32_t row = u / (uint32_t)NC, phys = u % (uint32_t)NC;
-    const uint32_t c = (phys + (uint32_t)NC - ((row >> 1) % (uint32_t)NC)) % (uint32_t)NC;
-    dma_off[i] = row * S + c * 16u;
-  }
+  // row = 8i + (lane >> 3) and rot(row) = (4i + (lane >> 4)) % 8 depends on
+  // i only through its parity: two per-lane bases, the rest is scalar
+  static_assert(NC == 8 && NI == 8, "line DMA geometry");
+  const uint32_t dphys = lane & 7u;
+  const uint32_t dbase0 = (lane >> 3) * S + ((dphys + 8u - ((lane >> 4) & 7u)) & 7u) * 16u;
+  const uint32_t dbase1 = (lane >> 3) * S + ((dphys + 8u - ((4u + (lane >> 4)) & 7u)) & 7u) * 16u;
   const uint32_t rot = (lane >> 1) % (uint32_t)NC;
   TestConsts tcv = a.tc;
   asm volatile("" : "+v"(tcv.c0));
@@ -635,9 +648,13 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // (zeros) so every batch is NI instructions
   auto issue = [&](const u32x4& rsrc, uint32_t sh, uint32_t b) {
     if constexpr (VARIANT == 4) return;
+    const uint32_t sb = b * (uint32_t)kLine - sh;  // scalar part
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const uint32_t vo = (b < NB) ? dma_off[i] + b * (uint32_t)kLine - sh : 0xFFFFFFF0u;
+      // the opaque scalar sum keeps LICM from hoisting 8 per-lane offsets
+      uint32_t ssum = (uint32_t)i * 8u * S + sb;
+      asm volatile("" : "+s"(ssum));
+      const uint32_t vo = (b < NB) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
       dma16(rsrc, vo, stage_lds + (uint32_t)i * 1024u);
     }
   };
@@ -674,7 +691,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 
     // wait for batch b, copy this lane's row to registers, issue batch b+1
     // (or the next region's warm-up line) into the freed staging line
-    auto fetch = [&](uint32_t b) {
+    auto fetch = [&](uint32_t b) __attribute__((always_inline)) {
       ++my_prog;
       s_prog[wave] = my_prog;
       const uint32_t their = s_prog[partner];
@@ -703,19 +720,89 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     // warm-up: the last 48 bytes before the segment fill the window (no test)
     hash_span<kRound, 0, false, MODE, VARIANT, SUB>(w + 20, h, ring, lds, slot8, tcv, lane, 0u,
                                                     cnt, ereg, myslots, 0u);
+    // Steady state: trips of 3 lines (384 B = 8 windows, so ring slots are
+    // static) as 48 subgroups of 8 bytes.  The table lookups run one subgroup
+    // ahead, ACROSS line boundaries: once the last subgroup of a line has
+    // issued its lookups, w is free, so the next line is copied in and its
+    // first lookups are issued before that last subgroup is hashed.
+    static_assert(SUB == 8, "trip pipeline is written for 8-byte subgroups");
+    uint64_t L[2][8];
+    auto issue_sub = [&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = (g % 16) * 8 + q;  // byte within the line
+        const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8);
+        const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot8, sel);
+        L[g & 1][q] = *reinterpret_cast<const uint64_t*>(lds + addr);
+      }
+    };
+    auto compute_sub = [&](auto gc, uint32_t o0) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr (VARIANT == 3) {  // staging-only ablation: keep the data live
+        h ^= w[(g % 16) * 2] ^ w[(g % 16) * 2 + 1];
+        asm volatile("" ::"v"(h));
+        return;
+      }
+      lookups_landed<8>(L[g & 1]);
+      constexpr bool kTest = VARIANT == 0 || VARIANT == 4;
+      uint32_t t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int rk = (g * 8 + q) % 48;
+        h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31),
+                                        (uint32_t)L[g & 1][q], ring[rk], 0x96);
+        ring[rk] = (uint32_t)(L[g & 1][q] >> 32);
+        if constexpr (kTest) {
+          if constexpr (MODE == 2) t[q] = mode2_t_mad(h, tcv.inv, (uint64_t)tcv.tadd);
+          else t[q] = is_cand<MODE>(h, tcv) ? 0u : 0xFFFFFFFFu;
+        }
+      }
+      if constexpr (!kTest) {
+        asm volatile("" ::"v"(h));
+      } else {
+        const uint32_t thr = MODE == 2 ? tcv.vmax : 1u;
+        uint32_t mn = t[0];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) mn = __builtin_elementwise_min(mn, t[q]);
+        if (__builtin_expect(__ballot(mn < thr) != 0, 0)) {
+          uint32_t bits = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if constexpr (MODE == 2) bits |= (mode2_exact(t[q], tcv) ? 1u : 0u) << q;
+            else bits |= (t[q] == 0u ? 1u : 0u) << q;
+          }
+          if (bits) {
+            const uint32_t e = (bits << 16) | (o0 + (uint32_t)(g * 8));
+#pragma unroll
+            for (int q = 0; q < kHitRegs; ++q) ereg[q] = cnt == (uint32_t)q ? e : ereg[q];
+            if (cnt >= (uint32_t)kHitRegs && cnt - kHitRegs < a.lane_slots)
+              myslots[cnt - kHitRegs] = e;
+            ++cnt;
+          }
+        }
+      }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    fetch(1u);
+    issue_sub(I0{});
     for (uint32_t t = 0; t < M; ++t) {
       const uint32_t o0 = t * 3u * (uint32_t)kLine;
-      fetch(3u * t + 1u);
-      hash_span<kLine, 0, true, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane, o0, cnt,
-                                                    ereg, myslots, a.lane_slots);
-      fetch(3u * t + 2u);
-      hash_span<kLine, 32, true, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane,
-                                                     o0 + kLine, cnt, ereg, myslots,
-                                                     a.lane_slots);
-      fetch(3u * t + 3u);
-      hash_span<kLine, 16, true, MODE, VARIANT, SUB>(w, h, ring, lds, slot8, tcv, lane,
-                                                     o0 + 2u * kLine, cnt, ereg, myslots,
-                                                     a.lane_slots);
+      static_for<48>([&](auto gc) __attribute__((always_inline)) {
+        constexpr int g = decltype(gc)::value;
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (g + 1 < 48) {
+          if constexpr ((g + 1) % 16 == 0) fetch(3u * t + 1u + (uint32_t)((g + 1) / 16));
+          issue_sub(std::integral_constant<int, g + 1>{});
+        } else {
+          if (t + 1 < M) {
+            fetch(3u * t + 4u);
+            issue_sub(I0{});
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        compute_sub(gc, o0);
+      });
     }
 
     // ---- region end: compact the lanes' hits into one sorted region list ----
