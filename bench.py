@@ -66,7 +66,8 @@ def make_blob(ctx, t, offset, n, workload):
 
 def load_traffic(workload, nbytes):
     """HBM bytes per scan launch from the committed rocprofv3 PMC pass
-    (profiles/traffic_<workload>.json, FETCH_SIZE x2 gfx950 correction)."""
+    (profiles/traffic_<workload>.json: L2 -> fabric read requests x their
+    sizes, tools/traffic_json.py)."""
     path = os.path.join(REPO, "profiles", f"traffic_{workload}.json")
     try:
         with open(path) as f:
