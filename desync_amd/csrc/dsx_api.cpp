@@ -109,8 +109,10 @@ struct dsx_ctx {
   bool scan_line = true;              // DSX_SCAN_LINE=0: 96-B-row scan_kernel instead of scanl_kernel
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
+  uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
+  uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
-  DevBuf<uint64_t> trace;       // [3 * trace_n scan records][7 * trace_walk_n walk records]
+  DevBuf<uint64_t> trace;       // [3 * trace_n scan records][10 * trace_walk_n walk records]
   uint64_t trace_n = 0, trace_walk_n = 0;
   uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
 
@@ -327,6 +329,8 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
   if (const char* v = getenv("DSX_SCAN_TRACE")) c->scan_trace = atoi(v) != 0;
+  if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
+  if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_LANE_TARGET"))
     c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
@@ -391,7 +395,7 @@ extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64
   if (!c || !n_scan || !n_walk) return DSX_E_INVAL;
   *n_scan = c->trace_n;
   *n_walk = c->trace_walk_n;
-  const uint64_t words = 3 * c->trace_n + 7 * c->trace_walk_n;
+  const uint64_t words = 3 * c->trace_n + 10 * c->trace_walk_n;
   if (!words || !out) return DSX_OK;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -552,7 +556,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   c->last_grid_P = line ? P - delta : P;
   if (c->scan_trace && line) {
     c->trace_n = (uint64_t)c->ncu * W;
-    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n + 7 * 65536));
+    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n + 10 * 65536));
     HIPCHK(c, hipMemsetAsync(c->trace.p, 0, 3 * c->trace_n * sizeof(uint64_t), c->stream));
     sa.trace = c->trace.p;
   }
@@ -632,7 +636,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.pc.overflow = sa.overflow;
   // the carried cut lies in (P - max, P] (its successor needed bytes >= P)
   const uint64_t anchor = (P > cc.origin + p->max) ? P - p->max : cc.origin;
-  const uint64_t seg = std::max<uint64_t>(4 * p->max, 1ull << 20);
+  const uint64_t seg = std::max<uint64_t>(c->seg_max_mult * p->max, c->seg_floor);
   const uint64_t end = is_last ? cc.L : P + len;
   const uint64_t nseg = end > anchor ? (end - anchor + seg - 1) / seg : 1;
   ta.anchor = anchor;

@@ -44,7 +44,8 @@ struct LdsSrc {
     const uint64_t ar = a - lo;  // a >= lo always (a = s+min, s >= lo)
     while (j < n && (uint64_t)c[j] <= ar) ++j;
     if (j < n) {
-      const uint64_t p = lo + c[j];
+      // (the builtin returns int: keep the u32 offset from sign-extending)
+      const uint64_t p = lo + (uint32_t)__builtin_amdgcn_readfirstlane(c[j]);
       if (p <= b) return p;
     }
     return kNone;
@@ -67,34 +68,46 @@ struct LdsSrc {
 struct WaveLdsSrc {
   const uint32_t* c;
   uint32_t n;
-  uint32_t j;
+  uint32_t base;  // window start: lane l holds c[base + l] in v
   uint64_t lo;
   uint32_t lane;
-  // j <- first index with c[j] > ar (or n)
-  __device__ void advance(uint64_t ar) {
-    while (j < n) {
-      const uint32_t idx = j + lane;
-      const uint32_t v = idx < n ? c[idx] : 0xFFFFFFFFu;
-      const uint64_t m = __ballot((uint64_t)v > ar || idx >= n);
+  uint32_t v;
+  __device__ void load() { v = base + lane < n ? c[base + lane] : 0xFFFFFFFFu; }
+  // first candidate > a (relative ar), searching forward from the window;
+  // returns its relative offset or 0xFFFFFFFF.  Steps of a chain advance by
+  // about one candidate, so most calls hit the window already in registers.
+  __device__ uint32_t next_after(uint64_t ar) {
+    const uint32_t ar32 = ar > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)ar;
+    while (true) {
+      const uint64_t m = __ballot(v > ar32);
       if (m) {
-        j += (uint32_t)__builtin_ctzll(m);
-        if (j > n) j = n;
-        return;
+        const uint32_t f = (uint32_t)__builtin_ctzll(m);
+        if (base + f >= n) return 0xFFFFFFFFu;
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)f);
       }
-      j += 64;
+      if (base + 64u >= n) return 0xFFFFFFFFu;
+      base += 64u;
+      load();
     }
   }
   __device__ uint64_t first_in(uint64_t a, uint64_t b) {
-    advance(a - lo);  // a >= lo always (a = s+min, s >= lo)
-    if (j < n) {
-      const uint64_t p = lo + c[j];
+    const uint32_t r = next_after(a - lo);  // a >= lo always (a = s+min, s >= lo)
+    if (r != 0xFFFFFFFFu) {
+      const uint64_t p = lo + r;
       if (p <= b) return p;
     }
     return kNone;
   }
+  // position the window at the first candidate > a
   __device__ void seek(uint64_t a) {
-    j = 0;
-    advance(a < lo ? 0 : a - lo);
+    base = 0;
+    load();
+    const uint64_t ar = a < lo ? 0 : a - lo;
+    const uint32_t ar32 = ar > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)ar;
+    while (base + 64u < n && __ballot(v > ar32) == 0) {
+      base += 64u;
+      load();
+    }
   }
 };
 
@@ -193,11 +206,11 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   __shared__ uint32_t s_off[kWalkMaxRegions + 1];
   __shared__ uint32_t s_wave[kWalkThreads / 64];
 
-  uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 7ull * blockIdx.x : nullptr;
+  uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 10ull * blockIdx.x : nullptr;
   if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
   const DevState* st = a.state;
   if (st->done || *a.pc.overflow) return;  // finished, or scan lists overflowed
-  const uint64_t s0 = st->carry;
+  const uint64_t s0 = uniform64(st->carry);  // scalar: the walks below are wave-uniform
   const uint32_t kA = blockIdx.x * a.spg;
   if (kA >= a.nseg) return;
   const uint32_t kB = (kA + a.spg < a.nseg ? kA + a.spg : a.nseg) - 1;  // inclusive
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   }
 
   const uint32_t nwalk = kB - kFirst + 1;
-  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   constexpr uint32_t kWaves = kWalkThreads / 64;
   // ---- phase 1: speculative chain of each segment -> exit X_k (one wave each) ----
   if (!dense) {
@@ -261,16 +274,21 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
       const uint32_t k = kFirst + t;
       const uint64_t v = seg_start(a, s0, k);
       const uint64_t e = seg_end(a, k);
-      WaveLdsSrc src{cand, total, 0, lo, ln};
+      WaveLdsSrc src{cand, total, 0, lo, ln, 0};
       src.seek(v);
+      if (tr && t == wv) tr[7] = __builtin_amdgcn_s_memrealtime();
       uint64_t x = v, last = v;
+      uint32_t steps = 0;
       while (true) {
         if (a.chain.is_last && x >= a.chain.L) break;
         const uint64_t nx = next_cut(x, src, a.chain);
+        if (tr && t == wv && steps == 0) tr[8] = __builtin_amdgcn_s_memrealtime();
+        ++steps;
         if (nx == kUndet || nx > e) break;
         last = nx;
         x = nx;
       }
+      if (tr && t == wv) tr[9] = __builtin_amdgcn_s_memrealtime();
       if (ln == 0) {
         xs[t] = last;
         if (k >= kA) a.seg_info[k].X = last;  // kA-1 belongs to the previous workgroup
@@ -298,10 +316,10 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
       }
       continue;
     }
-    const uint64_t E = (k == 0) ? s0 : xs[t - 1];
+    const uint64_t E = (k == 0) ? s0 : uniform64(xs[t - 1]);
     const uint64_t sst = seg_start(a, s0, k);
     const uint64_t e = seg_end(a, k);
-    WaveLdsSrc src{cand, total, 0, lo, ln};
+    WaveLdsSrc src{cand, total, 0, lo, ln, 0};
     src.seek(E);
     uint64_t* out = a.stage + (uint64_t)k * a.scap;
     uint32_t n = 0, flags = 0;

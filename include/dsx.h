@@ -200,8 +200,8 @@ int dsx_selftest_boundary(dsx_ctx_t *ctx, const dsx_params_t *p, int mode, uint6
  * {start, end, regions} of the line-aligned scan, then *n_walk stitch-walk
  * workgroup records {entry, counts scanned, candidates staged, speculative
  * walks done, staged walks done, s_memtime at staged, s_memtime at
- * speculative walks done}.  Copies min(cap, 3*n_scan + 7*n_walk) words to
- * out. */
+ * speculative walks done, first walk: seek done, first step done, chain
+ * done}.  Copies min(cap, 3*n_scan + 10*n_walk) words to out. */
 int dsx_debug_trace(dsx_ctx_t *ctx, uint64_t *out, uint64_t cap, uint64_t *n_scan,
                     uint64_t *n_walk);
 

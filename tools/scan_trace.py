@@ -25,13 +25,16 @@ _lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 1), ctx
 for i in range(3):
     print(f"scan_trace: call {i}", flush=True)
     desync_amd.cut_device(t.data_ptr(), n, 16384, 65536, 262144, ctx=ctx)
+st = ctx.stats()
+print(f"stats: chunks {st.chunks} candidates {st.candidates} repaired {st.repaired_segments} "
+      f"dense {st.dense_fallbacks}")
 ns, nw = ctypes.c_uint64(), ctypes.c_uint64()
 _lib.check(L.dsx_debug_trace(ctx.h, None, 0, ctypes.byref(ns), ctypes.byref(nw)), ctx.h)
-buf = np.zeros(3 * ns.value + 7 * nw.value, np.uint64)
+buf = np.zeros(3 * ns.value + 10 * nw.value, np.uint64)
 _lib.check(L.dsx_debug_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(ns),
                              ctypes.byref(nw)), ctx.h)
 tr = buf[:3 * ns.value].reshape(-1, 3).astype(np.int64)
-wk = buf[3 * ns.value:].reshape(-1, 7).astype(np.int64)
+wk = buf[3 * ns.value:].reshape(-1, 10).astype(np.int64)
 tr = tr[tr[:, 1] > 0]
 t0 = tr[:, 0].min()
 st = (tr[:, 0] - t0) / 100.0  # us (100 MHz)
@@ -51,3 +54,6 @@ if len(wk):
     print(f"walk workgroups {len(wk)} (times from the first scan wave start, us)")
     for i, name in enumerate(["entry", "counts", "staged", "walk1", "walk2"]):
         print(f"  {name:7s} pct {q} {np.percentile(rel[:, i], q).round(1).tolist()}")
+    sub = (wk[:, 7:10] - t0) / 100.0
+    for i, name in enumerate(["seek", "step1", "chain"]):
+        print(f"  {name:7s} pct {q} {np.percentile(sub[:, i], q).round(1).tolist()}")
