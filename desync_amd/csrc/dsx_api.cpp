@@ -30,7 +30,7 @@ template <class H>
 __global__ void digest_kernel(DigestArgs a);
 template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ void scan_kernel(ScanArgs a);
-template <int MODE, int VARIANT, int W, int SUB>
+template <int MODE, int VARIANT, int W, int SUB, int D>
 __global__ void scanl_kernel(ScanArgs a);
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
@@ -588,23 +588,23 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
     else                                                                                   \
       hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
   } while (0)
-#define DSX_LAUNCHL(WV, SUB)                                                              \
+#define DSX_LAUNCHL(WV, SUB, D)                                                           \
   do {                                                                                    \
     if (c->variant == 1)                                                                  \
-      hipLaunchKernelGGL((scanl_kernel<2, 1, WV, SUB>), g, b, 0, c->stream, sa);          \
+      hipLaunchKernelGGL((scanl_kernel<2, 1, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (c->variant == 3)                                                             \
-      hipLaunchKernelGGL((scanl_kernel<2, 3, WV, SUB>), g, b, 0, c->stream, sa);          \
+      hipLaunchKernelGGL((scanl_kernel<2, 3, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (c->variant == 4)                                                             \
-      hipLaunchKernelGGL((scanl_kernel<2, 4, WV, SUB>), g, b, 0, c->stream, sa);          \
+      hipLaunchKernelGGL((scanl_kernel<2, 4, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (mode == 2)                                                                   \
-      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB>), g, b, 0, c->stream, sa);          \
+      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (mode == 1)                                                                   \
-      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB>), g, b, 0, c->stream, sa);          \
+      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else                                                                                  \
-      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB>), g, b, 0, c->stream, sa);          \
+      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
   } while (0)
     if (line) {
-      DSX_LAUNCHL(8, 8);
+      DSX_LAUNCHL(8, 8, 1);
     } else switch (c->scan_cfg) {
       case 1: DSX_LAUNCH(1, 2, 12, 4, false); break;
       case 2: DSX_LAUNCH(1, 2, 16, 4, false); break;

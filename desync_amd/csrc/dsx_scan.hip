@@ -549,7 +549,7 @@ DSX_SCAN_INST(2, 1, 16, 4, false)
 // ring phases apart from the next (128 = 2*48 + 32), so the steady-state loop
 // runs three batches with phases 0, 32, 16.
 // ---------------------------------------------------------------------------
-template <int MODE, int VARIANT, int W, int SUB>
+template <int MODE, int VARIANT, int W, int SUB, int D>
 __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   constexpr int NC = kLine / 16;             // 16-B chunks per lane row
   constexpr int NI = kWave * kLine / 1024;   // DMA wave instructions per batch
@@ -725,8 +725,12 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     // ahead, ACROSS line boundaries: once the last subgroup of a line has
     // issued its lookups, w is free, so the next line is copied in and its
     // first lookups are issued before that last subgroup is hashed.
+    // D = lookup distance in subgroups (D + 1 lookup buffers; 48 % (D+1) == 0
+    // keeps the buffer index static across trips)
     static_assert(SUB == 8, "trip pipeline is written for 8-byte subgroups");
-    uint64_t L[2][8];
+    static_assert(D >= 1 && D <= 15 && 48 % (D + 1) == 0, "lookup distance");
+    constexpr int NL = D + 1;
+    uint64_t L[NL][8];
     auto issue_sub = [&](auto gc) __attribute__((always_inline)) {
       constexpr int g = decltype(gc)::value;
 #pragma unroll
@@ -734,7 +738,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         const int k = (g % 16) * 8 + q;  // byte within the line
         const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8);
         const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot8, sel);
-        L[g & 1][q] = *reinterpret_cast<const uint64_t*>(lds + addr);
+        L[g % NL][q] = *reinterpret_cast<const uint64_t*>(lds + addr);
       }
     };
     auto compute_sub = [&](auto gc, uint32_t o0) __attribute__((always_inline)) {
@@ -744,15 +748,15 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         asm volatile("" ::"v"(h));
         return;
       }
-      lookups_landed<8>(L[g & 1]);
+      lookups_landed<8>(L[g % NL]);
       constexpr bool kTest = VARIANT == 0 || VARIANT == 4;
       uint32_t t[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int rk = (g * 8 + q) % 48;
         h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31),
-                                        (uint32_t)L[g & 1][q], ring[rk], 0x96);
-        ring[rk] = (uint32_t)(L[g & 1][q] >> 32);
+                                        (uint32_t)L[g % NL][q], ring[rk], 0x96);
+        ring[rk] = (uint32_t)(L[g % NL][q] >> 32);
         if constexpr (kTest) {
           if constexpr (MODE == 2) t[q] = mode2_t_mad(h, tcv.inv, (uint64_t)tcv.tadd);
           else t[q] = is_cand<MODE>(h, tcv) ? 0u : 0xFFFFFFFFu;
@@ -783,21 +787,21 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         }
       }
     };
-    using I0 = std::integral_constant<int, 0>;
     fetch(1u);
-    issue_sub(I0{});
+    static_for<D>([&](auto gc) __attribute__((always_inline)) { issue_sub(gc); });
     for (uint32_t t = 0; t < M; ++t) {
       const uint32_t o0 = t * 3u * (uint32_t)kLine;
       static_for<48>([&](auto gc) __attribute__((always_inline)) {
         constexpr int g = decltype(gc)::value;
+        constexpr int gi = g + D;  // subgroup whose lookups are issued now
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (g + 1 < 48) {
-          if constexpr ((g + 1) % 16 == 0) fetch(3u * t + 1u + (uint32_t)((g + 1) / 16));
-          issue_sub(std::integral_constant<int, g + 1>{});
+        if constexpr (gi < 48) {
+          if constexpr (gi % 16 == 0) fetch(3u * t + 1u + (uint32_t)(gi / 16));
+          issue_sub(std::integral_constant<int, gi>{});
         } else {
-          if (t + 1 < M) {
-            fetch(3u * t + 4u);
-            issue_sub(I0{});
+          if (t + 1 < M) {  // the next trip's first subgroups
+            if constexpr (gi == 48) fetch(3u * t + 4u);
+            issue_sub(std::integral_constant<int, gi - 48>{});
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -869,14 +873,14 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   }
 }
 
-#define DSX_SCANL_INST(W, SUB)                                         \
-  template __global__ void scanl_kernel<0, 0, W, SUB>(ScanArgs);       \
-  template __global__ void scanl_kernel<1, 0, W, SUB>(ScanArgs);       \
-  template __global__ void scanl_kernel<2, 0, W, SUB>(ScanArgs);       \
-  template __global__ void scanl_kernel<2, 1, W, SUB>(ScanArgs);       \
-  template __global__ void scanl_kernel<2, 3, W, SUB>(ScanArgs);       \
-  template __global__ void scanl_kernel<2, 4, W, SUB>(ScanArgs);
-DSX_SCANL_INST(8, 8)
+#define DSX_SCANL_INST(W, SUB, D)                                       \
+  template __global__ void scanl_kernel<0, 0, W, SUB, D>(ScanArgs);     \
+  template __global__ void scanl_kernel<1, 0, W, SUB, D>(ScanArgs);     \
+  template __global__ void scanl_kernel<2, 0, W, SUB, D>(ScanArgs);     \
+  template __global__ void scanl_kernel<2, 1, W, SUB, D>(ScanArgs);     \
+  template __global__ void scanl_kernel<2, 3, W, SUB, D>(ScanArgs);     \
+  template __global__ void scanl_kernel<2, 4, W, SUB, D>(ScanArgs);
+DSX_SCANL_INST(8, 8, 1)  // D = 2 needs 16 more VGPRs than the 256 of two waves per SIMD
 
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1
 // (the plain form of chunker_test.go:190-213).  Diagnostic entry point.
