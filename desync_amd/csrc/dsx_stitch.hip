@@ -90,6 +90,19 @@ struct WaveLdsSrc {
       load();
     }
   }
+  __device__ uint32_t next_after32(uint32_t ar32) {
+    while (true) {
+      const uint64_t m = __ballot(v > ar32);
+      if (m) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(m);
+        if (base + f >= n) return 0xFFFFFFFFu;
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)f);
+      }
+      if (base + 64u >= n) return 0xFFFFFFFFu;
+      base += 64u;
+      load();
+    }
+  }
   __device__ uint64_t first_in(uint64_t a, uint64_t b) {
     const uint32_t r = next_after(a - lo);  // a >= lo always (a = s+min, s >= lo)
     if (r != 0xFFFFFFFFu) {
@@ -116,6 +129,44 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
+}
+
+// The chain rule in 32-bit coordinates relative to a walk workgroup's `lo`
+// (its candidates and segments span far less than 4 GiB): every chain step is
+// a handful of scalar 32-bit operations instead of 64-bit vector compares.
+constexpr uint32_t kRelUndet = 0xFFFFFFFFu;
+constexpr uint32_t kRelClamp = 0xFFFFFFF0u;
+struct RelChain {
+  uint32_t min, max, L, PE;  // L, PE relative to lo, clamped to kRelClamp
+  bool is_last;
+};
+__device__ __forceinline__ uint32_t rel_clamp(uint64_t v, uint64_t lo) {
+  return v <= lo ? 0u : (v - lo >= kRelClamp ? kRelClamp : (uint32_t)(v - lo));
+}
+__device__ __forceinline__ RelChain rel_chain(const ChainParams& w, uint64_t lo) {
+  // min/max clamped to 2^30: a walk workgroup spans far less, so a bound
+  // beyond 2^30 decides exactly like the real one (the chain leaves the
+  // segment either way), and s + max never overflows 32 bits
+  RelChain r;
+  r.min = w.min < (1ull << 30) ? (uint32_t)w.min : (1u << 30);
+  r.max = w.max < (1ull << 30) ? (uint32_t)w.max : (1u << 30);
+  r.L = rel_clamp(w.L, lo);
+  r.PE = rel_clamp(w.PE, lo);
+  r.is_last = w.is_last != 0;
+  return r;
+}
+// next(s) of chunker.go:206-277 for a relative chain position s (< L when
+// is_last); kRelUndet if the successor depends on bytes beyond the piece
+__device__ __forceinline__ uint32_t rel_next(uint32_t s, WaveLdsSrc& src, const RelChain& w) {
+  uint32_t lim = s + w.max;
+  if (w.is_last) {
+    if (w.L - s <= w.min) return w.L;  // chunker.go:215-217
+    if (lim > w.L) lim = w.L;          // chunker.go:221
+  }
+  const uint32_t c = src.next_after32(s + w.min);  // chunker.go:259-271
+  if (c <= lim) return c;                          // (none = 0xFFFFFFFF > lim)
+  if (!w.is_last && lim > w.PE) return kRelUndet;
+  return lim;  // chunker.go:276
 }
 
 // Candidates straight from the scan's per-region sorted lists (global
@@ -266,6 +317,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   }
 
   const uint32_t nwalk = kB - kFirst + 1;
+  const RelChain rc = rel_chain(a.chain, lo);
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   constexpr uint32_t kWaves = kWalkThreads / 64;
   // ---- phase 1: speculative chain of each segment -> exit X_k (one wave each) ----
@@ -277,21 +329,22 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
       WaveLdsSrc src{cand, total, 0, lo, ln, 0};
       src.seek(v);
       if (tr && t == wv) tr[7] = __builtin_amdgcn_s_memrealtime();
-      uint64_t x = v, last = v;
+      const uint32_t er = rel_clamp(e, lo);
+      uint32_t x = rel_clamp(v, lo), last = x;
       uint32_t steps = 0;
       while (true) {
-        if (a.chain.is_last && x >= a.chain.L) break;
-        const uint64_t nx = next_cut(x, src, a.chain);
+        if (rc.is_last && x >= rc.L) break;
+        const uint32_t nx = rel_next(x, src, rc);
         if (tr && t == wv && steps == 0) tr[8] = __builtin_amdgcn_s_memrealtime();
         ++steps;
-        if (nx == kUndet || nx > e) break;
+        if (nx == kRelUndet || nx > er) break;
         last = nx;
         x = nx;
       }
       if (tr && t == wv) tr[9] = __builtin_amdgcn_s_memrealtime();
       if (ln == 0) {
-        xs[t] = last;
-        if (k >= kA) a.seg_info[k].X = last;  // kA-1 belongs to the previous workgroup
+        xs[t] = lo + last;
+        if (k >= kA) a.seg_info[k].X = lo + last;  // kA-1 belongs to the previous workgroup
       }
     }
   }
@@ -323,14 +376,15 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     src.seek(E);
     uint64_t* out = a.stage + (uint64_t)k * a.scap;
     uint32_t n = 0, flags = 0;
-    uint64_t x = E, last = E;
+    const uint32_t er = rel_clamp(e, lo), sr = rel_clamp(sst, lo);
+    uint32_t x = rel_clamp(E, lo), last = x;
     while (true) {
-      if (a.chain.is_last && x >= a.chain.L) { flags |= kSegEnd; break; }
-      const uint64_t nx = next_cut(x, src, a.chain);
-      if (nx == kUndet) { flags |= kSegUndet; break; }
-      if (nx > e) break;
-      if (nx > sst) {
-        if (ln == (n & 63u) && n < a.scap) out[n] = nx;  // spread the stores over lanes
+      if (rc.is_last && x >= rc.L) { flags |= kSegEnd; break; }
+      const uint32_t nx = rel_next(x, src, rc);
+      if (nx == kRelUndet) { flags |= kSegUndet; break; }
+      if (nx > er) break;
+      if (nx > sr) {
+        if (ln == (n & 63u) && n < a.scap) out[n] = lo + nx;  // spread the stores over lanes
         ++n;
       }
       last = nx;
@@ -339,7 +393,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     if (n > a.scap) flags |= kSegOverflow;
     if (ln == 0) {
       si.E = E;
-      si.Z = last;
+      si.Z = lo + last;
       si.cnt = n;
       si.flags = flags;
     }
