@@ -112,6 +112,7 @@ struct dsx_ctx {
   uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
+  bool wave_major = true;             // DSX_WAVE_MAJOR: scanl's first regions wave-major
   DevBuf<uint64_t> trace;       // [3 * trace_n scan records][10 * trace_walk_n walk records]
   uint64_t trace_n = 0, trace_walk_n = 0;
   uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
@@ -329,6 +330,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
   if (const char* v = getenv("DSX_SCAN_TRACE")) c->scan_trace = atoi(v) != 0;
+  if (const char* v = getenv("DSX_WAVE_MAJOR")) c->wave_major = atoi(v) != 0;
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_LANE_TARGET"))
@@ -543,6 +545,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   sa.queue = c->overflow.p + 2 + (seq & 1);
   sa.queue_next = c->overflow.p + 2 + ((seq + 1) & 1);
   sa.state_init = c->init_pending ? (void*)c->state.p : nullptr;
+  sa.wave_major = c->wave_major ? 1u : 0u;
   sa.init_carry = c->init_carry;
   if (line) {
     // region 0's descriptor: the warm-up line unless it would start before

@@ -71,6 +71,8 @@ struct ScanArgs {
   uint32_t delta;
   uint32_t shift0;
   uint64_t* trace;       // diagnostics (DSX_SCAN_TRACE): per wave slot {start, end, regions}
+  uint32_t wave_major;   // first regions wave-major over the grid (DSX_WAVE_MAJOR, default 1)
+  uint32_t pad_;
 };
 
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches

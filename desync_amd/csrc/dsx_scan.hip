@@ -659,7 +659,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     }
   };
 
-  uint32_t region = blockIdx.x * W + wave;
+  // wave-major first regions: when regions do not fill every wave slot, the
+  // idle slots are single waves spread over many CUs (whose partner wave then
+  // runs alone, faster) instead of whole CUs at the end of the grid
+  uint32_t region = a.wave_major ? wave * gridDim.x + blockIdx.x : blockIdx.x * W + wave;
   if (region >= a.nregions) return;
   const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
   uint32_t nreg_done = 0;
