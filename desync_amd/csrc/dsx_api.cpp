@@ -65,7 +65,7 @@ namespace {
 constexpr uint64_t kPieceMax = 8ull << 30;       // bytes per scan launch
 constexpr uint64_t kHostChunk = 256ull << 20;    // host-resident pipeline chunk
 constexpr uint64_t kStreamBatch = 16ull << 20;   // streaming: bytes per device batch
-constexpr uint32_t kWalkLdsCap = 12288;          // candidates per walk workgroup
+constexpr uint32_t kWalkLdsCap = 8192;           // candidates per walk workgroup (2 workgroups per CU)
 constexpr uint32_t kDenseS = 48 * 9;             // dense path lane bytes (= slot cap)
 constexpr uint64_t kDensePiece = 32ull << 20;    // dense path piece size
 

@@ -256,6 +256,12 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   uint64_t* xs = (uint64_t*)(smem + a.lds_cap);  // [kMaxSpg + 1] spec exits
   __shared__ uint32_t s_off[kWalkMaxRegions + 1];
   __shared__ uint32_t s_wave[kWalkThreads / 64];
+  // phase 1's speculative chains (relative cuts), so phase 2 can stop as soon
+  // as its chain meets them: the rest of the staged chain is the same cuts
+  constexpr uint32_t kSpecLds = 4096;
+  __shared__ uint32_t s_spec[kSpecLds];
+  __shared__ uint32_t s_spec_n[kMaxSpg + 1];    // cuts recorded (capped at scap)
+  __shared__ uint32_t s_spec_end[kMaxSpg + 1];  // 0: left the segment, 1: reached L, 2: undetermined
 
   uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 10ull * blockIdx.x : nullptr;
   if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
@@ -318,6 +324,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
 
   const uint32_t nwalk = kB - kFirst + 1;
   const RelChain rc = rel_chain(a.chain, lo);
+  const bool record = nwalk * a.scap <= kSpecLds;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   constexpr uint32_t kWaves = kWalkThreads / 64;
   // ---- phase 1: speculative chain of each segment -> exit X_k (one wave each) ----
@@ -331,19 +338,25 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
       if (tr && t == wv) tr[7] = __builtin_amdgcn_s_memrealtime();
       const uint32_t er = rel_clamp(e, lo);
       uint32_t x = rel_clamp(v, lo), last = x;
-      uint32_t steps = 0;
+      uint32_t steps = 0, ns = 0, why = 0;
+      uint32_t* spec = s_spec + t * a.scap;
       while (true) {
-        if (rc.is_last && x >= rc.L) break;
+        if (rc.is_last && x >= rc.L) { why = 1; break; }
         const uint32_t nx = rel_next(x, src, rc);
         if (tr && t == wv && steps == 0) tr[8] = __builtin_amdgcn_s_memrealtime();
         ++steps;
-        if (nx == kRelUndet || nx > er) break;
+        if (nx == kRelUndet) { why = 2; break; }
+        if (nx > er) break;
+        if (record && ln == 0 && ns < a.scap) spec[ns] = nx;
+        ++ns;
         last = nx;
         x = nx;
       }
       if (tr && t == wv) tr[9] = __builtin_amdgcn_s_memrealtime();
       if (ln == 0) {
         xs[t] = lo + last;
+        s_spec_n[t] = ns <= a.scap ? ns : 0xFFFFFFFFu;  // overflow: no shortcut
+        s_spec_end[t] = why;
         if (k >= kA) a.seg_info[k].X = lo + last;  // kA-1 belongs to the previous workgroup
       }
     }
@@ -378,6 +391,10 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     uint32_t n = 0, flags = 0;
     const uint32_t er = rel_clamp(e, lo), sr = rel_clamp(sst, lo);
     uint32_t x = rel_clamp(E, lo), last = x;
+    // the speculative chain of this segment (phase 1), if recorded
+    const uint32_t sn = record ? s_spec_n[t] : 0xFFFFFFFFu;
+    const uint32_t* spec = s_spec + t * a.scap;
+    uint32_t sp = 0;  // first spec cut not below the staged chain
     while (true) {
       if (rc.is_last && x >= rc.L) { flags |= kSegEnd; break; }
       const uint32_t nx = rel_next(x, src, rc);
@@ -389,6 +406,21 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
       }
       last = nx;
       x = nx;
+      if (sn != 0xFFFFFFFFu) {
+        while (sp < sn && spec[sp] < nx) ++sp;
+        if (sp < sn && spec[sp] == nx) {
+          // met the speculative chain (all its cuts are > sst): the staged
+          // chain continues with its cuts and ends the way it ended
+          const uint32_t rest = sn - sp - 1;
+          for (uint32_t q = ln; q < rest; q += 64)
+            if (n + q < a.scap) out[n + q] = lo + spec[sp + 1 + q];
+          n += rest;
+          if (rest) last = spec[sn - 1];
+          if (s_spec_end[t] == 1) flags |= kSegEnd;
+          if (s_spec_end[t] == 2) flags |= kSegUndet;
+          break;
+        }
+      }
     }
     if (n > a.scap) flags |= kSegOverflow;
     if (ln == 0) {
