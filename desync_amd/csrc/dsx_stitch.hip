@@ -450,7 +450,8 @@ __device__ void publish(const StitchArgs& a, const DevState* st) {
   h->done = st->done;
   h->err = st->err;
   h->seq = a.seq;
-  __threadfence_system();
+  // (no system fence: the host reads this after the stream synchronises, and
+  // the end-of-kernel release makes the writes visible)
 }
 
 __device__ uint32_t bsearch_u64(const uint64_t* v, uint32_t n, uint64_t x) {
@@ -466,7 +467,9 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
   __shared__ uint32_t s_flag_cnt;
   __shared__ uint64_t s_part[kFixThreads / 64];
   __shared__ int s_last_seg;
+  __shared__ uint64_t s_carry, s_total0;
   DevState* st = a.state;
+  if (threadIdx.x == 0) s_total0 = st->total;
   if (st->done || *a.pc.overflow) {
     if (threadIdx.x == 0) {
       st->active = 0;
@@ -567,12 +570,18 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
   const uint32_t k1 = (k0 + per < T) ? k0 + per : T;
   uint64_t mine = 0;
   int last_nonempty = -1;
+  uint64_t my_last = 0;  // last cut of this thread's last non-empty segment
   for (uint32_t k = k0; k < k1; ++k) {
     const SegInfo& si = a.seg_info[k];
     const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
-    const uint64_t c = (uint64_t)a.rep_cnt[k] + (scnt - a.rep_from[k]);
+    const uint32_t rc = a.rep_cnt[k], rf = a.rep_from[k];
+    const uint64_t c = (uint64_t)rc + (scnt - rf);
     mine += c;
-    if (c > 0) last_nonempty = (int)k;
+    if (c > 0) {
+      last_nonempty = (int)k;
+      my_last = scnt > rf ? a.stage[(uint64_t)k * a.scap + scnt - 1]
+                          : a.rep[(uint64_t)k * a.scap + rc - 1];
+    }
   }
   if (threadIdx.x == 0) s_last_seg = -1;
   // wave-level inclusive scan, then a scan over the 16 wave totals
@@ -596,26 +605,21 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
     st->piece_cuts = acc;
   }
   __syncthreads();
-  uint64_t off = st->total + s_part[wv] + (incl - mine);
+  uint64_t off = s_total0 + s_part[wv] + (incl - mine);
   for (uint32_t k = k0; k < k1; ++k) {
     const SegInfo& si = a.seg_info[k];
     const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
     a.out_off[k] = off;
     off += (uint64_t)a.rep_cnt[k] + (scnt - a.rep_from[k]);
   }
+  // the owner of the last non-empty segment hands its last cut to thread 0
+  if (last_nonempty >= 0 && last_nonempty == s_last_seg) s_carry = my_last;
   __syncthreads();
   if (threadIdx.x == 0) {
     const int ls = s_last_seg;
-    if (ls >= 0) {
-      const SegInfo& si = a.seg_info[ls];
-      const uint32_t scnt = (si.flags & kBad) ? 0u : si.cnt;
-      uint64_t last;
-      if (scnt > a.rep_from[ls]) last = a.stage[(uint64_t)ls * a.scap + scnt - 1];
-      else last = a.rep[(uint64_t)ls * a.scap + a.rep_cnt[ls] - 1];
-      st->carry = last;
-    }
+    if (ls >= 0) st->carry = s_carry;
     if (a.chain.is_last && st->carry >= a.chain.L) st->done = 1;
-    const uint64_t tot = st->total + st->piece_cuts;
+    const uint64_t tot = s_total0 + st->piece_cuts;
     if (tot > a.out_cap) st->err |= kErrCapacity;
     st->total = tot;
     st->active = 1;
