@@ -65,6 +65,7 @@ namespace {
 constexpr uint64_t kPieceMax = 8ull << 30;       // bytes per scan launch
 constexpr uint64_t kHostChunk = 256ull << 20;    // host-resident pipeline chunk
 constexpr uint64_t kStreamBatch = 16ull << 20;   // streaming: bytes per device batch
+constexpr uint32_t kQueueDepth = 8;              // DSX_NO_SYNC calls queued per context
 constexpr uint32_t kWalkLdsCap = 8192;           // candidates per walk workgroup (2 workgroups per CU)
 constexpr uint32_t kDenseS = 48 * 9;             // dense path lane bytes (= slot cap)
 constexpr uint64_t kDensePiece = 32ull << 20;    // dense path piece size
@@ -162,14 +163,23 @@ struct dsx_ctx {
   std::vector<hipEvent_t> pev;
   uint32_t npiece_call = 0;
 
-  // pending DSX_NO_SYNC call (re-run synchronously on the dense path if needed)
+  // queued DSX_NO_SYNC calls, oldest first (each is re-run synchronously on
+  // the dense path if needed).  They run in order on the ctx stream and each
+  // publishes its chain state into its own pinned slot of h_ring.
   struct Pending {
-    bool active = false;
     const void* d_blob = nullptr;
     uint64_t len = 0, cap = 0;
     dsx_params_t p{};
     uint64_t* out = nullptr;
-  } pend;
+    uint32_t slot = 0;
+    uint64_t seq = 0;       // piece sequence number of the call's last piece
+    hipEvent_t done = nullptr;
+  };
+  std::deque<Pending> pend;
+  HostState* h_ring = nullptr;   // pinned, kQueueDepth slots
+  HostState* h_cur = nullptr;    // slot the next enqueued piece publishes into
+  hipEvent_t q_ev[kQueueDepth] = {};
+  uint32_t q_next = 0;
 };
 
 // Grow a device buffer; outstanding work may still use the old allocation, so
@@ -349,6 +359,11 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     CREATE_STEP(hipEventCreateWithFlags(&c->comp_done[i], hipEventDisableTiming));
   }
   CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
+  CREATE_STEP(hipHostMalloc((void**)&c->h_ring, kQueueDepth * sizeof(HostState)));
+  memset(c->h_ring, 0, kQueueDepth * sizeof(HostState));
+  c->h_cur = c->h_state;
+  for (uint32_t i = 0; i < kQueueDepth; ++i)
+    CREATE_STEP(hipEventCreateWithFlags(&c->q_ev[i], hipEventDisableTiming));
   CREATE_STEP(hipHostMalloc((void**)&c->h_res, 4 * sizeof(uint64_t)));
   memset(c->h_state, 0, sizeof(HostState));
   CREATE_STEP(c->state.ensure(1));
@@ -374,6 +389,9 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   c->dbuf[0].release(); c->dbuf[1].release();
   for (auto& p : c->pinned) if (p) (void)hipHostFree(p);
   if (c->h_state) (void)hipHostFree(c->h_state);
+  if (c->h_ring) (void)hipHostFree(c->h_ring);
+  for (uint32_t i = 0; i < kQueueDepth; ++i)
+    if (c->q_ev[i]) (void)hipEventDestroy(c->q_ev[i]);
   hipEvent_t evs[] = {c->ev_t0, c->ev_t1, c->ev_t2, c->copy_done[0], c->copy_done[1],
                       c->comp_done[0], c->comp_done[1]};
   for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
@@ -673,7 +691,7 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
   ta.out = cc.d_out;
   ta.out_cap = cc.out_cap;
   ta.state = c->state.p;
-  ta.host_state = c->h_state;
+  ta.host_state = c->h_cur;
   ta.seq = seq;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
   if (c->scan_trace && line && walk_grid <= 65536) {
@@ -755,17 +773,39 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
 
 extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
   if (!c || !n_out) return DSX_E_INVAL;
-  if (!c->pend.active) return DSX_E_STATE;
-  c->pend.active = false;
-  bool dense = false;
-  int rc = finish_call(c, n_out, c->pend.cap, &dense);
-  if (dense) {  // rare: redo on the dense-candidate path, synchronously
-    c->stats.dense_fallbacks++;
-    dsx_params_t p = c->pend.p;
-    return dsx_cut_device(c, c->pend.d_blob, c->pend.len, &p, c->pend.out, c->pend.cap, n_out,
-                          DSX_OUT_DEVICE);
+  if (c->pend.empty()) return DSX_E_STATE;
+  const dsx_ctx::Pending q = c->pend.front();
+  c->pend.pop_front();
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventSynchronize(q.done));
+  HostState s;
+  memcpy(&s, (const void*)&c->h_ring[q.slot], sizeof(HostState));
+  if (s.seq != q.seq) {
+    c->err = "stale chain state (queued call did not complete)";
+    return DSX_E_INTERNAL;
   }
-  return rc;
+  if (s.err & kErrDense) {  // rare: redo on the dense-candidate path, synchronously
+    c->stats.dense_fallbacks++;
+    dsx_params_t p = q.p;
+    return dsx_cut_device(c, q.d_blob, q.len, &p, q.out, q.cap, n_out, DSX_OUT_DEVICE);
+  }
+  c->stats.chunks = s.total;
+  c->stats.repaired_segments = s.repaired;
+  if (c->pend.empty()) {  // timing events belong to the last enqueued call
+    float scan = 0, stitch = 0;
+    for (uint32_t i = 0; i < c->npiece_call; ++i) {
+      float a = 0, b = 0;
+      (void)hipEventElapsedTime(&a, c->pev[3 * i], c->pev[3 * i + 1]);
+      (void)hipEventElapsedTime(&b, c->pev[3 * i + 1], c->pev[3 * i + 2]);
+      scan += a;
+      stitch += b;
+    }
+    c->stats.scan_ms = scan;
+    c->stats.stitch_ms = stitch;
+  }
+  *n_out = s.total;
+  if ((s.err & kErrCapacity) || s.total > q.cap) return DSX_E_CAPACITY;
+  return DSX_OK;
 }
 
 extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, const dsx_params_t* p,
@@ -779,17 +819,28 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
   const bool dev_out = (flags & DSX_OUT_DEVICE) != 0;
   const uint64_t need = len / p->min + 2;
   if ((flags & DSX_NO_SYNC) && dev_out) {
+    if (c->pend.size() >= kQueueDepth) {
+      c->err = "too many queued DSX_NO_SYNC calls (collect them with dsx_result)";
+      return DSX_E_STATE;
+    }
     CallCfg cc{p, len, 0, kRound, out_ends, cap, false};
-    c->pend.active = true;
-    c->pend.d_blob = d_blob;
-    c->pend.len = len;
-    c->pend.cap = cap;
-    c->pend.p = *p;
-    c->pend.out = out_ends;
+    dsx_ctx::Pending q;
+    q.d_blob = d_blob;
+    q.len = len;
+    q.cap = cap;
+    q.p = *p;
+    q.out = out_ends;
+    q.slot = c->q_next++ % kQueueDepth;
+    q.done = c->q_ev[q.slot];
+    c->h_cur = &c->h_ring[q.slot];
     HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
     rc = run_device(c, (const uint8_t*)d_blob, len, cc);
+    c->h_cur = c->h_state;
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
+    HIPCHK(c, hipEventRecord(q.done, c->stream));
+    q.seq = c->piece_seq;
+    c->pend.push_back(q);
     return DSX_OK;
   }
   for (int attempt = 0; attempt < 2; ++attempt) {

@@ -95,7 +95,8 @@ int dsx_cancel(dsx_ctx_t *ctx);
 #define DSX_OUT_HOST 0u   /* out_ends is host memory */
 #define DSX_OUT_DEVICE 1u /* out_ends is device memory on the ctx's device */
 #define DSX_NO_SYNC 2u    /* (device output only) enqueue on the ctx stream and return;
-                             fetch the count with dsx_result() (which waits) */
+                             up to 8 such calls may be queued (they run in order);
+                             dsx_result() waits for the OLDEST and returns its count */
 
 /* Device-resident blob (HBM) -> cut list.  d_blob must stay valid until the
  * call (or, with DSX_NO_SYNC, dsx_sync()) returns.  If cap is too small the
@@ -104,8 +105,9 @@ int dsx_cancel(dsx_ctx_t *ctx);
 int dsx_cut_device(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, const dsx_params_t *p,
                    uint64_t *out_ends, uint64_t cap, uint64_t *n_out, uint32_t flags);
 int dsx_sync(dsx_ctx_t *ctx);
-/* Completes a DSX_NO_SYNC dsx_cut_device(): waits, then returns its status and
- * cut count (the device cut list is valid once this returns DSX_OK). */
+/* Completes the oldest queued DSX_NO_SYNC dsx_cut_device(): waits for it, then
+ * returns its status and cut count (its device cut list is valid once this
+ * returns DSX_OK).  DSX_E_STATE if no call is queued. */
 int dsx_result(dsx_ctx_t *ctx, uint64_t *n_out);
 
 /* Host-memory blob -> cut list (host).  Pipelined pinned H2D inside. */

@@ -398,3 +398,31 @@ def _shard_protocol(data, world, dev):
     for c in ctxs:
         c.close()
     return rounds
+
+
+def test_queued_no_sync_calls(dctx):
+    """Up to 8 DSX_NO_SYNC dsx_cut_device calls queued on one context run in
+    order; dsx_result returns them oldest first, each with its own count and
+    cut list (bench.py's jobs in flight)."""
+    import torch
+    import desync_amd
+    from desync_amd import _lib
+    L = _lib.lib()
+    p = desync_amd.Params(MIN, AVG, MAX)
+    blobs, refs, outs = [], [], []
+    for i in range(5):
+        arr = o.synth_uniform(40 + i, 0, (3 << 20) + 1000 * i)
+        blobs.append(torch_dev(arr))
+        refs.append(o.chunk_stream(arr, MIN, AVG, MAX))
+        outs.append(torch.empty(arr.size // MIN + 4, dtype=torch.int64, device="cuda"))
+    cnt = ctypes.c_uint64()
+    for t, out in zip(blobs, outs):
+        _lib.check(L.dsx_cut_device(dctx.h, ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                    ctypes.byref(p.c), ctypes.c_void_p(out.data_ptr()),
+                                    out.numel(), ctypes.byref(cnt),
+                                    _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC), dctx.h)
+    for ref, out in zip(refs, outs):
+        _lib.check(L.dsx_result(dctx.h, ctypes.byref(cnt)), dctx.h)
+        assert cnt.value == ref.size
+        assert np.array_equal(out[:cnt.value].cpu().numpy().astype(np.uint64), ref)
+    assert L.dsx_result(dctx.h, ctypes.byref(cnt)) == _lib.DSX_E_STATE
