@@ -12,7 +12,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdsx.so")
+LIB_PATH = os.environ.get("DSX_LIB_PATH") or os.path.join(HERE, "libdsx.so")  # (A/B runs)
 
 DSX_OUT_HOST = 0
 DSX_OUT_DEVICE = 1

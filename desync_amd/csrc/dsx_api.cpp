@@ -285,7 +285,6 @@ static TestConsts make_tc(const dsx_params_t* p) {
   // 0x400000*d offset and the -1 back into the exact 24-bit check.
   tc.c0 = 12582911.0f;
   tc.madc = p->discriminator - 1u - (p->discriminator << 22);
-  tc.pad = 0;
   // MODE 2 prefilter: with d = 2^k * dodd, h + 1 = d*m (1 <= m <= 2^32/d)
   // gives t = (h+1)*inv - 1 = 2^k*m - 1 < 2^k*floor(2^32/d) = vmax (exact
   // for odd d; for even d the rare path re-checks h % d == d-1)
@@ -293,7 +292,10 @@ static TestConsts make_tc(const dsx_params_t* p) {
   tc.tadd = p->inverse_odd - 1u;
   tc.vmax = (uint32_t)(((1ull << 32) / p->discriminator) << k);
   tc.dodd = p->discriminator >> k;
-  tc.pad2 = 0;
+  // scanl keeps ~h in the hash register (the same recurrence from ~0), so
+  // t + 1 = (h+1)*inv = (~h)*(2^32 - inv) is one v_mul_lo_u32
+  tc.ninv = 0u - p->inverse_odd;
+  tc.vmax1 = tc.vmax + 1u;
   return tc;
 }
 
@@ -617,6 +619,8 @@ static int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, 
       hipLaunchKernelGGL((scanl_kernel<2, 3, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (c->variant == 4)                                                             \
       hipLaunchKernelGGL((scanl_kernel<2, 4, WV, SUB, D>), g, b, 0, c->stream, sa);       \
+    else if (c->variant == 5)                                                             \
+      hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (mode == 2)                                                                   \
       hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (mode == 1)                                                                   \

@@ -30,7 +30,7 @@ struct TestConsts {
   uint32_t d;      // discriminator
   uint32_t dm1;    // d - 1
   uint32_t madc;   // MODE 1: d - 1 - (d << 22) (folds the float offset, see is_cand)
-  uint32_t pad;
+  uint32_t ninv;   // MODE 2, scanl: 2^32 - inv, so (~h)*ninv = (h+1)*inv = t + 1
   uint32_t inv;    // inverse of odd part of d mod 2^32
   uint32_t qmax;   // (2^32-1)/d - qbias
   uint32_t qbias;
@@ -40,7 +40,7 @@ struct TestConsts {
   uint32_t tadd;   // MODE 2: inv - 1, so t = h*inv + tadd = (h+1)*inv - 1
   uint32_t vmax;   // MODE 2: 2^k * floor(2^32/d); candidate => t < vmax
   uint32_t dodd;   // MODE 2: d >> k (h = (t - tadd) * dodd recovers h)
-  uint32_t pad2;
+  uint32_t vmax1;  // MODE 2, scanl: vmax + 1 (candidate => t + 1 < vmax1; d >= 3 keeps it < 2^32)
 };
 
 struct ScanArgs {

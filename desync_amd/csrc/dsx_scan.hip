@@ -628,7 +628,6 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   TestConsts tcv = a.tc;
   asm volatile("" : "+v"(tcv.c0));
   asm volatile("" : "+v"(tcv.madc));
-  if constexpr (MODE == 2) asm volatile("" : "+v"(tcv.inv));
 
   // Region r's descriptor starts at its warm-up line (grid-relative
   // r*RB - 128), shifted by shift0 for region 0 so it never precedes the
@@ -664,7 +663,11 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // runs alone, faster) instead of whole CUs at the end of the grid
   uint32_t region = a.wave_major ? wave * gridDim.x + blockIdx.x : blockIdx.x * W + wave;
   if (region >= a.nregions) return;
-  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  // VARIANT 5 (diagnostic, same results): the trace records shader-clock
+  // cycles from start to end and those spent waiting for the line DMA
+  const uint64_t t_start = VARIANT == 5 ? __builtin_amdgcn_s_memtime()
+                                        : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
+  uint64_t vm_wait = 0;
   uint32_t nreg_done = 0;
   u32x4 rsrc;
   uint32_t sh;
@@ -686,7 +689,9 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     uint32_t ereg[kHitRegs] = {};
     const uint64_t gl = (uint64_t)region * 64u + lane;
     uint32_t* myslots = a.lane_slot + gl * a.lane_slots;
-    uint32_t h = 0;
+    // MODE 2 keeps ~h: rotl1(~x) == ~rotl1(x), so ~h follows the same
+    // recurrence from ~0, and t + 1 = (h+1)*inv = (~h)*ninv (make_tc)
+    uint32_t h = MODE == 2 ? ~0u : 0u;
     uint32_t ring[48];
 #pragma unroll
     for (int k = 0; k < 48; ++k) ring[k] = 0;
@@ -698,7 +703,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       ++my_prog;
       s_prog[wave] = my_prog;
       const uint32_t their = s_prog[partner];
+      uint64_t tw = 0;
+      if constexpr (VARIANT == 5) tw = __builtin_amdgcn_s_memtime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (VARIANT == 5) vm_wait += __builtin_amdgcn_s_memtime() - tw;
       const uint8_t* my_row = stage + lane * (uint32_t)kLine;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -752,7 +760,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         return;
       }
       lookups_landed<8>(L[g % NL]);
-      constexpr bool kTest = VARIANT == 0 || VARIANT == 4;
+      constexpr bool kTest = VARIANT == 0 || VARIANT == 4 || VARIANT == 5;
       uint32_t t[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -761,14 +769,14 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
                                         (uint32_t)L[g % NL][q], ring[rk], 0x96);
         ring[rk] = (uint32_t)(L[g % NL][q] >> 32);
         if constexpr (kTest) {
-          if constexpr (MODE == 2) t[q] = mode2_t_mad(h, tcv.inv, (uint64_t)tcv.tadd);
+          if constexpr (MODE == 2) t[q] = h * tcv.ninv;  // t + 1: one v_mul_lo_u32
           else t[q] = is_cand<MODE>(h, tcv) ? 0u : 0xFFFFFFFFu;
         }
       }
       if constexpr (!kTest) {
         asm volatile("" ::"v"(h));
       } else {
-        const uint32_t thr = MODE == 2 ? tcv.vmax : 1u;
+        const uint32_t thr = MODE == 2 ? tcv.vmax1 : 1u;
         uint32_t mn = t[0];
 #pragma unroll
         for (int q = 1; q < 8; ++q) mn = __builtin_elementwise_min(mn, t[q]);
@@ -776,7 +784,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
           uint32_t bits = 0;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            if constexpr (MODE == 2) bits |= (mode2_exact(t[q], tcv) ? 1u : 0u) << q;
+            if constexpr (MODE == 2) bits |= (mode2_exact(t[q] - 1u, tcv) ? 1u : 0u) << q;
             else bits |= (t[q] == 0u ? 1u : 0u) << q;
           }
           if (bits) {
@@ -871,8 +879,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   if (a.trace && lane == 0) {
     uint64_t* tr = a.trace + 3ull * (blockIdx.x * W + wave);
     tr[0] = t_start;
-    tr[1] = __builtin_amdgcn_s_memrealtime();
-    tr[2] = nreg_done;
+    tr[1] = VARIANT == 5 ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
+    tr[2] = VARIANT == 5 ? vm_wait : nreg_done;
   }
 }
 
@@ -882,7 +890,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   template __global__ void scanl_kernel<2, 0, W, SUB, D>(ScanArgs);     \
   template __global__ void scanl_kernel<2, 1, W, SUB, D>(ScanArgs);     \
   template __global__ void scanl_kernel<2, 3, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 4, W, SUB, D>(ScanArgs);
+  template __global__ void scanl_kernel<2, 4, W, SUB, D>(ScanArgs);     \
+  template __global__ void scanl_kernel<2, 5, W, SUB, D>(ScanArgs);
 DSX_SCANL_INST(8, 8, 1)  // D = 2 needs 16 more VGPRs than the 256 of two waves per SIMD
 
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1

@@ -36,6 +36,14 @@ _lib.check(L.dsx_debug_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(ns),
 tr = buf[:3 * ns.value].reshape(-1, 3).astype(np.int64)
 wk = buf[3 * ns.value:].reshape(-1, 10).astype(np.int64)
 tr = tr[tr[:, 1] > 0]
+if os.environ.get("DSX_SCAN_VARIANT") == "5":
+    # shader-clock cycles per wave and cycles spent waiting for the line DMA
+    tot = (tr[:, 1] - tr[:, 0]).astype(np.float64)
+    frac = tr[:, 2] / tot
+    q = [0, 10, 50, 90, 100]
+    print(f"waves {len(tr)}  DMA-wait fraction pct {q} {np.percentile(frac, q).round(3).tolist()}")
+    print(f"  cycles per wave median {np.median(tot):.0f}, waiting median {np.median(tr[:, 2]):.0f}")
+    sys.exit(0)
 t0 = tr[:, 0].min()
 st = (tr[:, 0] - t0) / 100.0  # us (100 MHz)
 en = (tr[:, 1] - t0) / 100.0
