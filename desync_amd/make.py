@@ -47,6 +47,9 @@ class NullProgressBar:
     def Set(self, current):
         pass
 
+    def Add(self, n):
+        pass
+
     def Finish(self):
         pass
 
@@ -191,3 +194,67 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
         finally:
             pb.Finish()
     return index, stats
+
+
+class VerifyError(Exception):
+    """The plain ``fmt.Errorf`` errors VerifyIndex returns (verifyindex.go:27,
+    fileseed.go:192)."""
+
+
+def _contiguous_runs(chunks):
+    """Split index chunks into runs whose chunks follow each other (a decoded
+    caibx is one run; a hand-built Index may have gaps or overlaps)."""
+    i = 0
+    while i < len(chunks):
+        j = i + 1
+        while j < len(chunks) and chunks[j].Start == chunks[j - 1].Start + chunks[j - 1].Size:
+            j += 1
+        yield chunks[i:j]
+        i = j
+
+
+def VerifyIndex(ctx, name, idx, n=1, pb=None, device=0):
+    """verifyindex.go:13-79 -- re-calculate the chunk IDs of a blob and compare
+    them with ``idx``.  Raises VerifyError on the first mismatch, as
+    fileSeedSegment.Validate does (fileseed.go:183-196).
+
+    The reference reads every chunk with ReadAt over ``n`` worker file handles;
+    here the file is read into HBM once and all IDs are computed by
+    dsx_chunk_ids (one launch per contiguous run of chunks).  ``n`` has no
+    effect on the result.  Block/char devices skip the size check
+    (verifyindex.go:26, isDevice)."""
+    import stat as _stat
+    pb = pb or NullProgressBar()
+    pb.SetTotal(len(idx.Chunks))
+    pb.Start()
+    try:
+        st = os.stat(name)
+        is_dev = _stat.S_ISBLK(st.st_mode) or _stat.S_ISCHR(st.st_mode)
+        if not is_dev and st.st_size != idx.Length():
+            raise VerifyError(f"index size ({idx.Length()}) does not match file size ({st.st_size})")
+        if ctx is not None and getattr(ctx, "done", lambda: False)():
+            return None  # the reference stops feeding workers and returns g.Wait()
+        if not idx.Chunks:
+            return None
+        need = max(c.Start + c.Size for c in idx.Chunks)
+        with open(name, "rb") as f:
+            size = os.fstat(f.fileno()).st_size if not is_dev else need
+            if need > size:
+                # ReadAt past the end of the file: io.EOF (fileseed.go:187)
+                raise EOFError("EOF")
+            dctx = _lib.default_context(device)
+            blob = _file_to_device(f, need, device)
+        for run in _contiguous_runs(idx.Chunks):
+            if ctx is not None and getattr(ctx, "done", lambda: False)():
+                break
+            start = run[0].Start
+            ends = np.fromiter((c.Start + c.Size for c in run), dtype=np.uint64, count=len(run))
+            ids = chunk_ids(blob.data_ptr(), need, ends, start, ctx=dctx)
+            for c, got in zip(run, ids):
+                if got != bytes(c.ID):
+                    raise VerifyError(f"seed index for {name} doesn't match its data")
+            pb.Add(len(run))
+        del blob
+    finally:
+        pb.Finish()
+    return None
