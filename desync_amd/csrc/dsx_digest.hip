@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dsx_digest.h"
 
 namespace dsx {
@@ -60,7 +62,41 @@ __constant__ uint32_t kK256[64] = {
 __constant__ uint32_t kIV256[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
 
-__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate / shift as two v_alignbit_b32 on the register halves (the
+// generic form costs two 64-bit shifts and two ORs).  n is a compile-time
+// constant after unrolling, so the n < 32 branch folds away.
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rlo, rhi;
+  if (n < 32) {
+    rlo = __builtin_amdgcn_alignbit(hi, lo, n);
+    rhi = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rhi << 32) | rlo;
+}
+__device__ __forceinline__ uint64_t shr64(uint64_t x, int n) {  // 0 < n < 32
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+}
+// three-input bit functions as one v_bitop3_b32 per dword (gfx950): 0x96 =
+// a^b^c, 0xE8 = majority(a,b,c) (both symmetric in their inputs)
+__device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t maj32(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return ((uint64_t)xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+         xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+__device__ __forceinline__ uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
+  return ((uint64_t)maj32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+         maj32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
@@ -84,26 +120,35 @@ struct Sha512 {
 #pragma unroll
     for (int i = 0; i < 16; ++i) W[i] = ((uint64_t)d[2 * i] << 32) | d[2 * i + 1];
     uint64_t a = H[0], b = H[1], c = H[2], e = H[4], f = H[5], g = H[6], h = H[7], dd = H[3];
+    // 80 rounds as 5 passes of 16 (the first without message expansion): the
+    // inner 16 are unrolled so every W index is static (no indexed register
+    // access), the outer loop stays rolled to keep the kernel small.
+    auto pass = [&](auto expand, int t0) {
+      constexpr bool EXPAND = decltype(expand)::value;
+      uint64_t K[16];  // this pass's constants: one wait
 #pragma unroll
-    for (int t = 0; t < 80; ++t) {
-      uint64_t w;
-      if (t < 16) {
-        w = W[t];
-      } else {
-        const uint64_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-        w = W[t & 15] + s0 + W[(t + 9) & 15] + s1;
-        W[t & 15] = w;
+      for (int j = 0; j < 16; ++j) K[j] = kK512[t0 + j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if constexpr (EXPAND) {
+          const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
+          const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+          const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
+          W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
+        }
+        const uint64_t w = W[j];
+        const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+        const uint64_t ch = (e & f) ^ (~e & g);
+        const uint64_t t1 = h + S1 + ch + K[j] + w;
+        const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+        const uint64_t maj = maj64(a, b, c);
+        const uint64_t t2 = S0 + maj;
+        h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
       }
-      const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-      const uint64_t ch = (e & f) ^ (~e & g);
-      const uint64_t t1 = h + S1 + ch + kK512[t] + w;
-      const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-      const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
-      const uint64_t t2 = S0 + maj;
-      h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
-    }
+    };
+    pass(std::false_type{}, 0);  // rounds 0-15: no message expansion
+#pragma unroll 1
+    for (int t0 = 16; t0 < 80; t0 += 16) pass(std::true_type{}, t0);
     H[0] += a; H[1] += b; H[2] += c; H[3] += dd; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
   }
   // SHA-512/256: the first 32 bytes of the big-endian state
@@ -130,26 +175,32 @@ struct Sha256 {
 #pragma unroll
     for (int i = 0; i < 16; ++i) W[i] = d[i];
     uint32_t a = H[0], b = H[1], c = H[2], dd = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+    auto pass = [&](auto expand, int t0) {
+      constexpr bool EXPAND = decltype(expand)::value;
+      uint32_t K[16];  // this pass's constants: one wait
 #pragma unroll
-    for (int t = 0; t < 64; ++t) {
-      uint32_t w;
-      if (t < 16) {
-        w = W[t];
-      } else {
-        const uint32_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
-        const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-        const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
-        w = W[t & 15] + s0 + W[(t + 9) & 15] + s1;
-        W[t & 15] = w;
+      for (int j = 0; j < 16; ++j) K[j] = kK256[t0 + j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if constexpr (EXPAND) {
+          const uint32_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
+          const uint32_t s0 = xor3_32(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+          const uint32_t s1 = xor3_32(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+          W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
+        }
+        const uint32_t w = W[j];
+        const uint32_t S1 = xor3_32(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+        const uint32_t ch = (e & f) ^ (~e & g);
+        const uint32_t t1 = h + S1 + ch + K[j] + w;
+        const uint32_t S0 = xor3_32(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+        const uint32_t maj = maj32(a, b, c);
+        const uint32_t t2 = S0 + maj;
+        h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
       }
-      const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-      const uint32_t ch = (e & f) ^ (~e & g);
-      const uint32_t t1 = h + S1 + ch + kK256[t] + w;
-      const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-      const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
-      const uint32_t t2 = S0 + maj;
-      h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
-    }
+    };
+    pass(std::false_type{}, 0);  // rounds 0-15: no message expansion
+#pragma unroll 1
+    for (int t0 = 16; t0 < 64; t0 += 16) pass(std::true_type{}, t0);
     H[0] += a; H[1] += b; H[2] += c; H[3] += dd; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
   }
   __device__ void out(uint8_t* dst) const {
@@ -159,44 +210,56 @@ struct Sha256 {
   }
 };
 
-// Full block at blob + pos (pos + BLK <= len): aligned dwordx4 loads over the
-// 16-byte-aligned window, re-aligned with v_alignbyte, big-endian assembled.
+// Full blocks come in two steps so the next block's loads are in flight
+// while the current one is compressed (one wave per SIMD at small blobs: the
+// load latency would otherwise sit on every block's critical path).
+// fetch_raw: the aligned dwordx4 loads over the 16-byte-aligned window of
+// [pos, pos + BLK); only valid when fast_ok(pos) (window inside the blob).
 template <int BLK>
-__device__ __forceinline__ void load_block(const uint8_t* blob, uint64_t pos, uint64_t len,
-                                           uint32_t (&d)[32]) {
+__device__ __forceinline__ bool fast_ok(uint64_t pos, uint64_t len) {
+  return (pos & ~15ull) + BLK + 16 <= len;
+}
+template <int BLK>
+__device__ __forceinline__ void fetch_raw(const uint8_t* blob, uint64_t pos, uint32_t (&raw)[BLK / 4 + 4]) {
   constexpr int ND = BLK / 4;
-  const uint64_t a0 = pos & ~15ull;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* p = reinterpret_cast<const u32x4*>(blob + (pos & ~15ull));
+#pragma unroll
+  for (int i = 0; i < ND / 4 + 1; ++i) {
+    const u32x4 v = __builtin_nontemporal_load(p + i);
+    raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
+  }
+}
+// align_raw: re-align with v_alignbyte and assemble big-endian dwords.
+template <int BLK>
+__device__ __forceinline__ void align_raw(const uint32_t (&raw)[BLK / 4 + 4], uint64_t pos,
+                                          uint32_t (&d)[32]) {
+  constexpr int ND = BLK / 4;
   const uint32_t sh = (uint32_t)(pos & 15u);
-  if (a0 + BLK + 16 <= len) {
-    uint32_t raw[ND + 4];
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4* p = reinterpret_cast<const u32x4*>(blob + a0);
+  const uint32_t dsh = sh >> 2, bsh = (sh & 3u) * 8u;
 #pragma unroll
-    for (int i = 0; i < ND / 4 + 1; ++i) {
-      const u32x4 v = __builtin_nontemporal_load(p + i);
-      raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
+  for (int i = 0; i < ND; ++i) {
+    // dword i of the block = bytes [pos + 4i, pos + 4i + 4): raw[dsh + i], raw[dsh + i + 1]
+    uint32_t lo = raw[i], hi = raw[i + 1];
+    // select by dsh (0..3) without dynamic register indexing
+#pragma unroll
+    for (int s = 1; s < 4; ++s) {
+      lo = dsh == (uint32_t)s ? raw[i + s] : lo;
+      hi = dsh == (uint32_t)s ? raw[i + s + 1] : hi;
     }
-    const uint32_t dsh = sh >> 2, bsh = (sh & 3u) * 8u;
-#pragma unroll
-    for (int i = 0; i < ND; ++i) {
-      // dword i of the block = bytes [pos + 4i, pos + 4i + 4): raw[dsh + i], raw[dsh + i + 1]
-      uint32_t lo = raw[i], hi = raw[i + 1];
-      // select by dsh (0..3) without dynamic register indexing
-#pragma unroll
-      for (int s = 1; s < 4; ++s) {
-        lo = dsh == (uint32_t)s ? raw[i + s] : lo;
-        hi = dsh == (uint32_t)s ? raw[i + s + 1] : hi;
-      }
-      const uint32_t v = bsh ? __builtin_amdgcn_alignbit(hi, lo, bsh) : lo;
-      d[i] = bswap32(v);
-    }
-  } else {  // near the blob end: byte loads
+    const uint32_t v = bsh ? __builtin_amdgcn_alignbit(hi, lo, bsh) : lo;
+    d[i] = bswap32(v);
+  }
+}
+// Near the blob end: byte loads.
+template <int BLK>
+__device__ __forceinline__ void load_block_bytes(const uint8_t* blob, uint64_t pos, uint32_t (&d)[32]) {
+  constexpr int ND = BLK / 4;
 #pragma unroll 4
-    for (int i = 0; i < ND; ++i) {
-      uint32_t v = 0;
-      for (int k = 0; k < 4; ++k) v = (v << 8) | blob[pos + 4 * i + k];
-      d[i] = v;
-    }
+  for (int i = 0; i < ND; ++i) {
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k) v = (v << 8) | blob[pos + 4 * i + k];
+    d[i] = v;
   }
 }
 
@@ -232,6 +295,8 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
   uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // first chunk: static
   uint64_t s = 0, e = 0, pos = 0;
   uint32_t phase = 0;  // 0 = data blocks, 1 = tail with marker, 2 = length-only block
+  uint32_t raw[BLK / 4 + 4];  // prefetched window of the next full block
+  bool have_next = false;
   H st;
   auto start_chunk = [&]() {
     if (ci < a.n) {
@@ -239,6 +304,7 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
       e = a.ends[ci];
       pos = s;
       phase = 0;
+      have_next = false;
       st.init();
     }
   };
@@ -249,11 +315,22 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
     if (__ballot(live) == 0) break;
     uint32_t d[32];
     bool finished = false;
+    have_next = have_next && live;
     if (live) {
       const uint64_t r = e - pos;
       if (phase == 0 && r >= (uint64_t)BLK) {
-        load_block<BLK>(a.blob, pos, a.len, d);
+        if (have_next) {
+          align_raw<BLK>(raw, pos, d);
+        } else if (fast_ok<BLK>(pos, a.len)) {
+          fetch_raw<BLK>(a.blob, pos, raw);
+          align_raw<BLK>(raw, pos, d);
+        } else {
+          load_block_bytes<BLK>(a.blob, pos, d);
+        }
         pos += BLK;
+        // prefetch the next full block of this chunk
+        have_next = e - pos >= (uint64_t)BLK && fast_ok<BLK>(pos, a.len);
+        if (have_next) fetch_raw<BLK>(a.blob, pos, raw);
       } else {
         const uint64_t bits = (e - s) * 8u;
         if (phase == 0) {
