@@ -1205,9 +1205,20 @@ extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uin
   }
   HIPCHK(c, c->dg_queue.ensure(1));
   HIPCHK(c, hipMemsetAsync(c->dg_queue.p, 0, 4, c->stream));
-  // lanes: up to 4 workgroups of 256 per CU, each lane pulls chunks from the queue
+  // Lanes: exactly the workgroups that are resident at once (occupancy is set
+  // by VGPRs: 2 per CU for SHA-512, 3 for SHA-256), every lane pulling chunks
+  // from the queue.  A larger grid would hand its non-resident workgroups a
+  // static share that starts only when the first wave of workgroups is done.
+  int per_cu = 0;
+  if (algo == DSX_DIGEST_SHA512_256)
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha512>,
+                                                           kDigestThreads, 0));
+  else
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha256>,
+                                                           kDigestThreads, 0));
+  if (per_cu < 1) per_cu = 1;
   const uint64_t blocks = std::min<uint64_t>((n + kDigestThreads - 1) / kDigestThreads,
-                                             4ull * (uint64_t)c->ncu);
+                                             (uint64_t)per_cu * (uint64_t)c->ncu);
   DigestArgs da{};
   da.blob = (const uint8_t*)d_blob;
   da.len = len;

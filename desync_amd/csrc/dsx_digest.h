@@ -20,6 +20,9 @@ struct DigestArgs {
   uint32_t pad;
 };
 
-constexpr int kDigestThreads = 256;
+#ifndef DSX_DIGEST_THREADS
+#define DSX_DIGEST_THREADS 256
+#endif
+constexpr int kDigestThreads = DSX_DIGEST_THREADS;
 
 }  // namespace dsx
