@@ -102,8 +102,11 @@ class Chunker:
             self._eof = True
             check(lib().dsx_stream_push(self.ctx.h, None, 0, 1), self.ctx.h)
             return
-        buf = ctypes.create_string_buffer(bytes(data), len(data))
-        check(lib().dsx_stream_push(self.ctx.h, buf, len(data), 0), self.ctx.h)
+        if not isinstance(data, bytes):
+            data = bytes(data)
+        # bytes are immutable and stay alive for the call: passed without a copy
+        # (the library copies what it keeps, dsx.h)
+        check(lib().dsx_stream_push(self.ctx.h, data, len(data), 0), self.ctx.h)
 
 
 def NewChunker(reader, min_size, avg_size, max_size, **kw):

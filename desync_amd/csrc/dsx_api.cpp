@@ -1081,7 +1081,9 @@ extern "C" int dsx_stream_push(dsx_ctx_t* c, const void* bytes, uint64_t len, in
   // compact: keep bytes from min(cur, scan_pos - 64)
   uint64_t keep_from = std::min(s.cur, s.scan_pos >= 64 ? s.scan_pos - 64 : 0);
   keep_from = std::max(keep_from, s.buf_pos);
-  if (keep_from > s.buf_pos) {
+  // Drop consumed bytes only once they are at least half the buffer: each
+  // byte is moved O(1) times instead of once per push.
+  if (keep_from > s.buf_pos && 2 * (keep_from - s.buf_pos) >= s.buf.size()) {
     s.buf.erase(s.buf.begin(), s.buf.begin() + (keep_from - s.buf_pos));
     s.buf_pos = keep_from;
   }
