@@ -45,7 +45,7 @@ EXPORTS = (
     "dsx_params_init", "dsx_strerror", "dsx_abi_version", "dsx_ctx_create", "dsx_ctx_destroy",
     "dsx_last_error", "dsx_cancel", "dsx_cut_device", "dsx_sync", "dsx_result", "dsx_cut_host",
     "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
-    "dsx_stream_done", "dsx_stream_chunk_data", "dsx_shard_local", "dsx_shard_resolve",
+    "dsx_stream_done", "dsx_stream_end", "dsx_stream_chunk_data", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace",
 )
@@ -136,6 +136,7 @@ def lib():
             "dsx_stream_pop": (i32, [vp, P(u64), P(u64)]),
             "dsx_stream_advance": (i32, [vp, u64]),
             "dsx_stream_done": (i32, [vp]),
+            "dsx_stream_end": (i32, [vp]),
             "dsx_stream_chunk_data": (vp, [vp]),
             "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), vp, u32]),
             "dsx_shard_resolve": (i32, [vp, vp, i32, i32, vp, vp, u64, P(u64), u32]),

@@ -49,7 +49,12 @@ class Chunker:
     def __init__(self, reader, min_size, avg_size, max_size, ctx=None, device=0):
         self.params = Params(min_size, avg_size, max_size)
         self.r = reader
-        self.ctx = ctx if ctx is not None else _lib.default_context(device)
+        # Like a Go Chunker (its own buffer and hash state, chunker.go:108-131)
+        # every Chunker owns a library context: the stream state and device
+        # scratch live there.  A caller-supplied ctx must not carry another
+        # unfinished stream (dsx_stream_begin refuses: DSX_E_STATE).
+        self._own = ctx is None
+        self.ctx = _lib.Context(device) if ctx is None else ctx
         check(lib().dsx_stream_begin(self.ctx.h, ctypes.byref(self.params.c)), self.ctx.h)
         self._eof = False
         self._start = ctypes.c_uint64()
@@ -82,6 +87,20 @@ class Chunker:
 
     def Max(self):
         return self.params.max
+
+    def close(self):
+        """Release the stream (and the context, if this Chunker created it)."""
+        if self.ctx is not None and self.ctx.h:
+            lib().dsx_stream_end(self.ctx.h)
+            if self._own:
+                self.ctx.close()
+        self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     # -- pythonic aliases --------------------------------------------------
     next = Next

@@ -996,6 +996,13 @@ extern "C" int dsx_cut_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, cons
 // --------------------------------------------------------------------------
 extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
   if (!c || !p) return DSX_E_INVAL;
+  // one stream per context (its scratch and carried state live here): a
+  // second Chunker on a context whose stream is still being read is refused
+  // instead of silently resetting the first one
+  if (c->st.active && !(c->st.done && c->st.cuts.empty())) {
+    c->err = "a stream is already active on this context (dsx_stream_end it first)";
+    return DSX_E_STATE;
+  }
   c->st = dsx_ctx::Stream();
   c->st.active = true;
   c->st.p = *p;
@@ -1114,6 +1121,12 @@ extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
 }
 
 extern "C" const uint8_t* dsx_stream_chunk_data(dsx_ctx_t* c) { return c ? c->st.last_chunk : nullptr; }
+
+extern "C" int dsx_stream_end(dsx_ctx_t* c) {
+  if (!c) return DSX_E_INVAL;
+  c->st = dsx_ctx::Stream();
+  return DSX_OK;
+}
 
 extern "C" int dsx_stream_done(dsx_ctx_t* c) {
   if (!c) return 0;

@@ -120,7 +120,11 @@ int dsx_cut_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, const dsx_par
                uint64_t *out_ends, uint64_t cap, uint64_t *n_out);
 
 /* ---- streaming (Chunker.Next / Advance over an io.Reader) -------------------
- * begin: resets the stream to position 0 with params p (NewChunker).
+ * One stream per context (a Chunker owns its context, as each Go Chunker owns
+ * its buffer and hash state, chunker.go:108-131).
+ * begin: starts a stream at position 0 with params p (NewChunker).  Returns
+ *        DSX_E_STATE while another stream on ctx is unfinished.
+ * end:   drops the stream state (the context can begin a new one).
  * push:  appends bytes read from the reader; eof=1 marks the end of input.
  *        The library copies the bytes (caller keeps ownership).
  * pop:   start and size of the next confirmed chunk.  Returns 1 if a chunk was
@@ -136,6 +140,7 @@ int dsx_stream_push(dsx_ctx_t *ctx, const void *bytes, uint64_t len, int eof);
 int dsx_stream_pop(dsx_ctx_t *ctx, uint64_t *start, uint64_t *size);
 int dsx_stream_advance(dsx_ctx_t *ctx, uint64_t n);
 int dsx_stream_done(dsx_ctx_t *ctx);
+int dsx_stream_end(dsx_ctx_t *ctx);
 /* Pointer to the bytes of the chunk returned by the last pop (host memory,
  * valid until the next push/pop/advance -- Next()'s aliasing rule,
  * chunker.go:202-205). */

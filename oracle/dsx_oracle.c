@@ -296,3 +296,65 @@ uint64_t dsxo_chunk_parallel(const uint8_t *buf, uint64_t len, const dsxo_params
     free(w); free(th);
     return k;
 }
+
+/* ---- synthetic inputs: CPU twins of desync_amd/csrc/dsx_gen.hip ------------
+ * These are not reference algorithms (the BASELINE configs only name the
+ * shapes: uniform bytes, 30 % repeated 1 MiB blocks); they let the tests
+ * regenerate any window of the device-generated workloads on the host and
+ * check the device bytes before comparing cut lists.  Stream definition:
+ *   uniform: 8-byte word i = splitmix64(seed * 2^40 + i), little endian;
+ *   dedup:   1 MiB blocks; block b > 0 is, with probability p, a copy of block
+ *            j = hi32(r) mod b (r = splitmix64(seed<<40 ^ b*K ^ C), taken when
+ *            lo32(r) < p_thresh), followed down to a fresh block; a fresh
+ *            block's bytes are the uniform stream's bytes of that block. */
+static inline uint64_t splitmix64(uint64_t z) {
+    z = z * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E5A1ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+uint32_t dsxo_dedup_thresh(double p_repeat) {
+    double t = p_repeat * 4294967296.0;
+    return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+uint64_t dsxo_dedup_root(uint64_t blk, uint64_t seed, uint32_t p_thresh) {
+    while (blk > 0) {
+        uint64_t r = splitmix64((seed << 40) ^ (blk * 0x2545F4914F6CDD1Dull) ^ 0xD1B54A32D192ED03ull);
+        if ((uint32_t)r >= p_thresh) break;
+        blk = (r >> 32) % blk;
+    }
+    return blk;
+}
+
+/* bytes [src, src+n) of the uniform stream of `seed` into dst */
+static void gen_uniform_at(uint8_t *dst, uint64_t src, uint64_t n, uint64_t seed) {
+    const uint64_t sb = seed << 40;
+    uint64_t i = 0;
+    while (i < n) {
+        const uint64_t a = src + i, w = splitmix64(sb + (a >> 3));
+        const unsigned s = (unsigned)(a & 7u);
+        if (s == 0 && n - i >= 8) {
+            memcpy(dst + i, &w, 8); /* little-endian host (x86-64) */
+            i += 8;
+        } else {
+            dst[i++] = (uint8_t)(w >> (8u * s));
+        }
+    }
+}
+
+void dsxo_gen_uniform(uint8_t *dst, uint64_t offset, uint64_t len, uint64_t seed) {
+    gen_uniform_at(dst, offset, len, seed);
+}
+
+void dsxo_gen_dedup(uint8_t *dst, uint64_t offset, uint64_t len, uint64_t seed, uint32_t p_thresh) {
+    uint64_t i = 0;
+    while (i < len) {
+        const uint64_t a = offset + i, blk = a >> 20, in = a & 0xFFFFFull;
+        const uint64_t n = (1ull << 20) - in < len - i ? (1ull << 20) - in : len - i;
+        const uint64_t root = dsxo_dedup_root(blk, seed, p_thresh);
+        gen_uniform_at(dst + i, (root << 20) | in, n, seed);
+        i += n;
+    }
+}

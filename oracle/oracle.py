@@ -117,6 +117,14 @@ def lib():
         L.dsxo_chain.argtypes = [p, u64, u64, u64, u64, p, u64]
         L.dsxo_chunk_parallel.restype = u64
         L.dsxo_chunk_parallel.argtypes = [p, u64, ctypes.POINTER(_Params), ctypes.c_int, p, u64]
+        L.dsxo_dedup_thresh.restype = u32
+        L.dsxo_dedup_thresh.argtypes = [ctypes.c_double]
+        L.dsxo_dedup_root.restype = u64
+        L.dsxo_dedup_root.argtypes = [u64, u64, u32]
+        L.dsxo_gen_uniform.restype = None
+        L.dsxo_gen_uniform.argtypes = [p, u64, u64, u64]
+        L.dsxo_gen_dedup.restype = None
+        L.dsxo_gen_dedup.argtypes = [p, u64, u64, u64, u32]
         _LIB = L
     return _LIB
 
@@ -346,3 +354,50 @@ def synth_uniform(seed, offset, length):
     b = words.view(np.uint8)
     s = offset - w0 * 8
     return b[s:s + length].copy()
+
+
+def default_threads():
+    """Host threads for the oracle: the GPU box exports OMP_NUM_THREADS (its
+    CPU share, 16); os.cpu_count() there reports the whole machine."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(n or 16, os.cpu_count() or 1))
+
+
+def _gen_parallel(fn, args, offset, length, out, threads):
+    import concurrent.futures as cf
+    a = np.empty(length, dtype=np.uint8) if out is None else out
+    assert a.size >= length and a.flags.c_contiguous
+    if length == 0:
+        return a
+    step = max(1 << 20, -(-length // (4 * threads)))
+    step = (step + 7) & ~7
+    with cf.ThreadPoolExecutor(max_workers=threads) as pool:
+        futs = [pool.submit(fn, a.ctypes.data + o, offset + o, min(step, length - o), *args)
+                for o in range(0, length, step)]
+        for f in futs:
+            f.result()
+    return a
+
+
+def synth_uniform_c(seed, offset, length, out=None, threads=None):
+    """synth_uniform in C (dsxo_gen_uniform) over host threads, for GiB sizes."""
+    return _gen_parallel(lib().dsxo_gen_uniform, (seed,), offset, length, out,
+                         threads or default_threads())
+
+
+def synth_dedup(seed, offset, length, p_repeat=0.30, out=None, threads=None):
+    """Bytes [offset, offset+length) of the dedup stream (BASELINE config 3
+    shape): the CPU twin of dsx_gen_dedup (desync_amd/csrc/dsx_gen.hip)."""
+    th = lib().dsxo_dedup_thresh(p_repeat)
+    return _gen_parallel(lib().dsxo_gen_dedup, (seed, th), offset, length, out,
+                         threads or default_threads())
+
+
+def dedup_roots(seed, nblocks, p_repeat=0.30):
+    """Source block of every 1 MiB block of the dedup stream (copy chains
+    followed down to a fresh block)."""
+    th = lib().dsxo_dedup_thresh(p_repeat)
+    return np.array([lib().dsxo_dedup_root(b, seed, th) for b in range(nblocks)], dtype=np.uint64)

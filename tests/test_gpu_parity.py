@@ -319,6 +319,41 @@ def test_stream_matches(dctx):
     assert ends == ref.tolist()
 
 
+def test_two_chunkers_interleaved(dctx):
+    """Each Chunker is independent: Next() alternated between two
+    streams over different data returns each stream's own chunks; a second
+    stream on a context whose stream is unfinished is refused."""
+    import desync_amd
+    from desync_amd import _lib
+    a = o.synth_uniform(12, 0, (9 << 20) + 11)
+    b = o.synth_uniform(13, 0, (7 << 20) + 5)
+    ca = desync_amd.NewChunker(io.BytesIO(a.tobytes()), MIN, AVG, MAX)
+    cb = desync_amd.NewChunker(io.BytesIO(b.tobytes()), 4096, 16384, 65536)
+    got_a, got_b = [], []
+    while True:
+        sa, xa = ca.Next()
+        sb, xb = cb.Next()
+        if xa:
+            got_a.append(sa + len(xa))
+        if xb:
+            got_b.append(sb + len(xb))
+        if not xa and not xb:
+            break
+    assert got_a == o.chunk_stream(a, MIN, AVG, MAX).tolist()
+    assert got_b == o.chunk_stream(b, 4096, 16384, 65536).tolist()
+    ctx = _lib.Context(0)
+    try:
+        c1 = desync_amd.NewChunker(io.BytesIO(a.tobytes()), MIN, AVG, MAX, ctx=ctx)
+        c1.Next()
+        with pytest.raises(_lib.DsxError):
+            desync_amd.NewChunker(io.BytesIO(b.tobytes()), MIN, AVG, MAX, ctx=ctx)
+        c1.close()
+        c2 = desync_amd.NewChunker(io.BytesIO(b.tobytes()), MIN, AVG, MAX, ctx=ctx)
+        assert [s + len(x) for s, x in c2] == o.chunk_stream(b, MIN, AVG, MAX).tolist()
+    finally:
+        ctx.close()
+
+
 # ---------------------------------------------------------------- BASELINE sizes
 def test_config2_1gib_uniform(dctx):
     """BASELINE config 2: 1 GiB uniform bytes (seed 1), default params + sweep."""
