@@ -1,0 +1,203 @@
+// dsx_engine.h -- host engine internals shared by the C-ABI translation
+// units (dsx_api.cpp: cut lists, streaming, shards; dsx_index.cpp: file ->
+// cut list + chunk IDs).  Not part of the ABI (include/dsx.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/dsx.h"
+#include "dsx_common.h"
+#include "dsx_digest.h"
+#include "dsx_stitch.h"
+
+namespace dsx {
+template <class H>
+__global__ void digest_kernel(DigestArgs a);
+template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
+__global__ void scan_kernel(ScanArgs a);
+template <int MODE, int VARIANT, int W, int SUB, int D>
+__global__ void scanl_kernel(ScanArgs a);
+__global__ void walk_kernel(StitchArgs a);
+__global__ void fixup_kernel(StitchArgs a);
+__global__ void gather_kernel(StitchArgs a);
+__global__ void gen_uniform_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed);
+__global__ void gen_dedup_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed,
+                                 uint32_t p_thresh);
+__global__ void boundary_selftest_kernel(TestConsts tc, int mode, uint64_t h0, uint64_t n,
+                                         unsigned long long* mismatches);
+__global__ void seam_cands_kernel(PieceCands pc, uint64_t lo, uint64_t wend, dsx_seam_t* seam);
+__global__ void seam_finalize_kernel(dsx_seam_t* seam, const uint64_t* cuts, const DevState* st,
+                                     uint64_t shard_start, uint64_t shard_len, uint64_t total,
+                                     uint64_t wend0, uint64_t entry, uint32_t flags);
+__global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
+                                    uint64_t max, uint64_t* ext, uint64_t* info);
+__global__ void shard_emit_kernel(const uint64_t* info, const uint64_t* ext, const uint64_t* spec,
+                                  uint64_t nspec, uint64_t* out, uint64_t cap, volatile uint64_t* res);
+}  // namespace dsx
+
+using namespace dsx;
+
+namespace dsx_host {
+
+constexpr uint64_t kPieceMax = 8ull << 30;       // bytes per scan launch
+constexpr uint64_t kHostChunk = 256ull << 20;    // host-resident pipeline chunk
+constexpr uint64_t kStreamBatch = 16ull << 20;   // streaming: bytes per device batch
+constexpr uint32_t kQueueDepth = 8;              // DSX_NO_SYNC calls queued per context
+constexpr uint32_t kWalkLdsCap = 8192;           // candidates per walk workgroup (2 workgroups per CU)
+constexpr uint32_t kDenseS = 48 * 9;             // dense path lane bytes (= slot cap)
+constexpr uint64_t kDensePiece = 32ull << 20;    // dense path piece size
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t want) {
+    if (want <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t sz = want < 16 ? 16 : want;
+    hipError_t e = hipMalloc((void**)&p, sz * sizeof(T));
+    if (e == hipSuccess) n = sz;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace dsx_host
+using namespace dsx_host;
+
+struct dsx_ctx {
+  int device = 0;
+  int ncu = 256;
+  hipStream_t stream = nullptr, copy_stream = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_t2 = nullptr;
+  hipEvent_t copy_done[2] = {nullptr, nullptr}, comp_done[2] = {nullptr, nullptr};
+  std::atomic<int> cancel{0};
+  std::string err;
+  int force_mode = -1;  // DSX_TEST_MODE env override
+  int variant = 0;      // DSX_SCAN_VARIANT: diagnostic scan ablations (wrong results)
+  uint32_t lane_bytes_override = 0;  // DSX_LANE_BYTES (tuning; multiple of 48)
+  int prefetch_batches = 0;           // DSX_PREFETCH: L2 prefetch distance in DMA batches (0 = off)
+  int regions_per_slot = 1;           // DSX_REGIONS_PER_SLOT: scan work units per wave slot
+  int scan_cfg = 0;                   // DSX_SCAN_CFG: index into kCfg* (waves, rounds/batch, LDS buffers)
+  bool scan_line = true;              // DSX_SCAN_LINE=0: 96-B-row scan_kernel instead of scanl_kernel
+  int scanl_waves = 8;                // waves per workgroup of scanl_kernel
+  uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
+  uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
+  uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
+  bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
+  bool wave_major = true;             // DSX_WAVE_MAJOR: scanl's first regions wave-major
+  DevBuf<uint64_t> trace;       // [3 * trace_n scan records][10 * trace_walk_n walk records]
+  uint64_t trace_n = 0, trace_walk_n = 0;
+  uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
+
+  DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
+  DevBuf<uint32_t> lane_slot;
+  DevBuf<SegInfo> seg_info;
+  DevBuf<uint64_t> stage, rep, out_off, out;
+  DevBuf<uint64_t> dg_ends;   // chunk IDs: staged chunk ends
+  DevBuf<uint8_t> dg_ids;     // chunk IDs: staged digests
+  DevBuf<uint32_t> dg_queue;  // chunk IDs: lane work queue
+  DevBuf<DevState> state;
+  DevBuf<uint8_t> dbuf[2];
+  uint8_t* pinned[2] = {nullptr, nullptr};
+  size_t pinned_sz = 0;
+  HostState* h_state = nullptr;  // pinned mirror published by fixup_kernel
+  uint64_t piece_seq = 0;        // global piece counter (overflow parity, freshness)
+  bool init_pending = false;     // next scan initialises DevState with init_carry
+  uint64_t last_region_bytes = 0;  // geometry of the last enqueued piece's region lists
+  uint32_t last_nregions = 0, last_region_cap = 0;
+  uint64_t init_carry = 0;
+
+  // streaming state (Chunker.Next over an io.Reader)
+  struct Stream {
+    bool active = false, eof = false, done = false;
+    dsx_params_t p{};
+    std::vector<uint8_t> buf;
+    uint64_t buf_pos = 0, scan_pos = 0, origin = 0, cur = 0, skip = 0, carry = 0;
+    std::deque<uint64_t> cuts;
+    const uint8_t* last_chunk = nullptr;
+  } st;
+
+  // multi-GPU shard state (dsx_shard_local -> dsx_shard_resolve)
+  struct Shard {
+    const uint8_t* d = nullptr;  // caller's shard bytes (valid until resolve returns OK)
+    uint64_t halo = 0, start = 0, len = 0, total = 0;
+    dsx_params_t p{};
+    uint64_t nspec = 0;  // speculative cuts in ctx->out
+    bool valid = false;
+  } sh;
+  DevBuf<dsx_seam_t> d_seam, d_all;
+  DevBuf<uint64_t> d_ext, d_info, d_emit;
+  uint64_t* h_res = nullptr;  // pinned: shard_emit_kernel status / count / entry
+
+  dsx_stats_t stats{};
+  // per-piece timing events of the current call: {before scan, after scan, after gather}
+  std::vector<hipEvent_t> pev;
+  uint32_t npiece_call = 0;
+
+  // queued DSX_NO_SYNC calls, oldest first (each is re-run synchronously on
+  // the dense path if needed).  They run in order on the ctx stream and each
+  // publishes its chain state into its own pinned slot of h_ring.
+  struct Pending {
+    const void* d_blob = nullptr;
+    uint64_t len = 0, cap = 0;
+    dsx_params_t p{};
+    uint64_t* out = nullptr;
+    uint32_t slot = 0;
+    uint64_t seq = 0;       // piece sequence number of the call's last piece
+    hipEvent_t done = nullptr;
+  };
+  std::deque<Pending> pend;
+  HostState* h_ring = nullptr;   // pinned, kQueueDepth slots
+  HostState* h_cur = nullptr;    // slot the next enqueued piece publishes into
+  hipEvent_t q_ev[kQueueDepth] = {};
+  uint32_t q_next = 0;
+};
+
+// Grow a device buffer; outstanding work may still use the old allocation, so
+// drain both streams before freeing it.  Allocates 25% headroom.
+template <class T>
+inline hipError_t grow(dsx_ctx* c, DevBuf<T>& b, size_t n) {
+  if (b.p && b.n >= n) return hipSuccess;
+  if (b.p) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->copy_stream);
+  }
+  return b.ensure(n + n / 4 + 64);
+}
+
+int set_hip_err(dsx_ctx* c, hipError_t e, const char* what);
+
+#define HIPCHK(ctx, expr)                                  \
+  do {                                                     \
+    hipError_t e_ = (expr);                                \
+    if (e_ != hipSuccess) return set_hip_err(ctx, e_, #expr); \
+  } while (0)
+
+struct CallCfg {
+  const dsx_params_t* p;
+  uint64_t L;        // blob length (final piece knows it)
+  uint64_t origin;   // chain origin: first cut position (0, Advance target, shard start)
+  uint64_t min_pos;  // candidates below this absolute position are not real windows
+  uint64_t* d_out;   // device output
+  uint64_t out_cap;
+  bool dense;        // dense-candidate path
+  uint64_t halo0 = 0;  // readable bytes before the first piece (shards)
+};
+
+// engine entry points (dsx_api.cpp)
+int reset_state(dsx_ctx* c, uint64_t carry);
+int read_state(dsx_ctx* c, HostState* out);
+int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_t halo,
+                  uint64_t P, uint64_t len, bool is_last);
+int ensure_attr_walk(dsx_ctx* c);
