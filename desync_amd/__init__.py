@@ -18,11 +18,12 @@ from .digest import SHA256, SHA512256, NewNullChunk, NullChunk, set_digest  # no
 from .errors import Interrupted  # noqa: F401
 from .index import FormatIndex, Index, IndexChunk, IndexFromReader  # noqa: F401
 from .make import ChunkingStats, IndexFromFile, VerifyError, VerifyIndex, chunk_ids, cut_device, cut_device_result, \
-    cut_fd, cut_host  # noqa: F401
+    cut_fd, cut_host, file_size, index_fd, index_host  # noqa: F401
 
 __all__ = [
     "ChunkerWindowSize", "Chunker", "NewChunker", "Params", "SHA256", "SHA512256", "NullChunk",
     "NewNullChunk", "set_digest", "Interrupted", "FormatIndex", "Index", "IndexChunk",
     "IndexFromReader", "ChunkingStats", "IndexFromFile", "cut_device", "cut_device_result",
-    "cut_fd", "cut_host", "chunk_ids", "VerifyIndex", "VerifyError",
+    "cut_fd", "cut_host", "chunk_ids", "VerifyIndex", "VerifyError", "file_size", "index_fd",
+    "index_host",
 ]

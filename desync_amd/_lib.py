@@ -47,7 +47,7 @@ EXPORTS = (
     "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
     "dsx_stream_done", "dsx_stream_end", "dsx_stream_chunk_data", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
-    "dsx_get_stats", "dsx_debug_trace",
+    "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -145,6 +145,8 @@ def lib():
             "dsx_gen_dedup": (i32, [vp, vp, u64, u64, u64, ctypes.c_double]),
             "dsx_chunk_ids": (i32, [vp, vp, u64, u64, vp, u64, vp, u32, i32]),
             "dsx_get_stats": (i32, [vp, P(Stats)]),
+            "dsx_index_fd": (i32, [vp, i32, u64, u64, P(Params), i32, vp, vp, u64, P(u64)]),
+            "dsx_index_host": (i32, [vp, vp, u64, P(Params), i32, vp, vp, u64, P(u64)]),
             "dsx_debug_trace": (i32, [vp, vp, u64, P(u64), P(u64)]),
         }
         for name, (res, args) in sig.items():
@@ -203,6 +205,7 @@ class Context:
 
 
 _default = {}
+_pool = {}  # device -> idle contexts (IndexFromFile is re-entrant, a context is not)
 
 
 def default_context(device=0):
@@ -211,3 +214,27 @@ def default_context(device=0):
         ctx = Context(device)
         _default[device] = ctx
     return ctx
+
+
+class pooled_context:
+    """``with pooled_context(dev) as ctx``: a context no other thread uses
+    meanwhile (created on demand, returned to a per-device pool afterwards;
+    the pipeline buffers a context holds are reused by the next call)."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self.ctx = None
+
+    def __enter__(self):
+        with _lock:
+            idle = _pool.setdefault(self.device, [])
+            self.ctx = idle.pop() if idle else None
+        if self.ctx is None:
+            self.ctx = Context(self.device)
+        return self.ctx
+
+    def __exit__(self, *exc):
+        with _lock:
+            _pool.setdefault(self.device, []).append(self.ctx)
+        self.ctx = None
+        return False

@@ -176,6 +176,9 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_LANE_TARGET"))
     c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
+  if (const char* v = getenv("DSX_INDEX_WINDOW")) c->index_window = (uint64_t)std::max(1L << 16, atol(v));
+  if (const char* v = getenv("DSX_INDEX_SLOT")) c->index_slot = (uint64_t)std::max(1L << 12, atol(v));
+  if (const char* v = getenv("DSX_INDEX_READERS")) c->index_readers = std::max(1, std::min(32, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
     const long lb = atol(v);
     if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
@@ -218,6 +221,7 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   c->d_seam.release(); c->d_all.release(); c->d_ext.release(); c->d_info.release(); c->d_emit.release();
   if (c->h_res) (void)hipHostFree(c->h_res);
   c->dbuf[0].release(); c->dbuf[1].release();
+  index_release(c);
   for (auto& p : c->pinned) if (p) (void)hipHostFree(p);
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
@@ -1015,6 +1019,39 @@ extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_
 // --------------------------------------------------------------------------
 // chunk IDs (Digest.Sum per chunk: digest.go:11-29, make.go:223)
 // --------------------------------------------------------------------------
+// Enqueues digest_kernel on the ctx stream.  max_n bounds the chunk count
+// (the grid is sized from it; with da.range_lo the count is read on the
+// device).
+int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo) {
+  // Lanes: exactly the workgroups that are resident at once (occupancy is set
+  // by VGPRs: 2 per CU for SHA-512, 3 for SHA-256), every lane pulling chunks
+  // from the queue.  A larger grid would hand its non-resident workgroups a
+  // static share that starts only when the first wave of workgroups is done.
+  int per_cu = 0;
+  if (algo == DSX_DIGEST_SHA512_256)
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha512>,
+                                                           kDigestThreads, 0));
+  else
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha256>,
+                                                           kDigestThreads, 0));
+  if (per_cu < 1) per_cu = 1;
+  const uint64_t blocks = std::max<uint64_t>(
+      1, std::min<uint64_t>((max_n + kDigestThreads - 1) / kDigestThreads,
+                            (uint64_t)per_cu * (uint64_t)c->ncu));
+  HIPCHK(c, c->dg_queue.ensure(1));
+  HIPCHK(c, hipMemsetAsync(c->dg_queue.p, 0, 4, c->stream));
+  da.queue = c->dg_queue.p;
+  da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * kDigestThreads);
+  if (algo == DSX_DIGEST_SHA512_256)
+    hipLaunchKernelGGL(digest_kernel<Sha512>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
+                       c->stream, da);
+  else
+    hipLaunchKernelGGL(digest_kernel<Sha256>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
+                       c->stream, da);
+  HIPCHK(c, hipGetLastError());
+  return DSX_OK;
+}
+
 extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uint64_t start,
                              const uint64_t* ends, uint64_t n, void* ids, uint32_t flags,
                              int algo) {
@@ -1024,6 +1061,19 @@ extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uin
   if ((flags & ~(DSX_OUT_DEVICE | DSX_ENDS_DEVICE)) != 0) return DSX_E_INVAL;
   if (n == 0) return DSX_OK;
   if (n > 0xFFFFFFF0ull) return DSX_E_INVAL;
+  if (!(flags & DSX_ENDS_DEVICE)) {
+    // chunks must lie inside the blob, in order (a hand-built index could
+    // otherwise send the kernel past the end of the buffer); device-resident
+    // ends are bounds-checked per chunk by the kernel instead
+    uint64_t prev = start;
+    for (uint64_t i = 0; i < n; ++i) {
+      if (ends[i] < prev || ends[i] > len) {
+        c->err = "chunk ends must be non-decreasing, start <= ends[0], ends[n-1] <= len";
+        return DSX_E_INVAL;
+      }
+      prev = ends[i];
+    }
+  }
   HIPCHK(c, hipSetDevice(c->device));
   c->err.clear();
   const uint64_t* d_ends = ends;
@@ -1037,22 +1087,6 @@ extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uin
     HIPCHK(c, grow(c, c->dg_ids, n * 32));
     d_ids = c->dg_ids.p;
   }
-  HIPCHK(c, c->dg_queue.ensure(1));
-  HIPCHK(c, hipMemsetAsync(c->dg_queue.p, 0, 4, c->stream));
-  // Lanes: exactly the workgroups that are resident at once (occupancy is set
-  // by VGPRs: 2 per CU for SHA-512, 3 for SHA-256), every lane pulling chunks
-  // from the queue.  A larger grid would hand its non-resident workgroups a
-  // static share that starts only when the first wave of workgroups is done.
-  int per_cu = 0;
-  if (algo == DSX_DIGEST_SHA512_256)
-    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha512>,
-                                                           kDigestThreads, 0));
-  else
-    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha256>,
-                                                           kDigestThreads, 0));
-  if (per_cu < 1) per_cu = 1;
-  const uint64_t blocks = std::min<uint64_t>((n + kDigestThreads - 1) / kDigestThreads,
-                                             (uint64_t)per_cu * (uint64_t)c->ncu);
   DigestArgs da{};
   da.blob = (const uint8_t*)d_blob;
   da.len = len;
@@ -1060,15 +1094,8 @@ extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uin
   da.first_start = start;
   da.n = n;
   da.ids = d_ids;
-  da.queue = c->dg_queue.p;
-  da.nfirst = (uint32_t)std::min<uint64_t>(n, blocks * kDigestThreads);
-  if (algo == DSX_DIGEST_SHA512_256)
-    hipLaunchKernelGGL(digest_kernel<Sha512>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
-                       c->stream, da);
-  else
-    hipLaunchKernelGGL(digest_kernel<Sha256>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
-                       c->stream, da);
-  HIPCHK(c, hipGetLastError());
+  int rc = launch_digest(c, da, n, algo);
+  if (rc) return rc;
   if (!(flags & DSX_OUT_DEVICE))
     HIPCHK(c, hipMemcpyAsync(ids, d_ids, n * 32, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

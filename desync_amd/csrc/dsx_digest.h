@@ -9,16 +9,28 @@ struct Sha512;  // SHA-512/256 (digest.go:22)
 struct Sha256;  // SHA-256 (digest.go:28)
 
 struct DigestArgs {
-  const uint8_t* blob;
-  uint64_t len;
-  const uint64_t* ends;  // [n] chunk end offsets (device)
-  uint64_t first_start;  // start of chunk 0
+  const uint8_t* blob;   // blob[0] is absolute position base_off
+  uint64_t len;          // readable bytes at blob
+  const uint64_t* ends;  // [n] chunk end offsets, absolute (device)
+  uint64_t first_start;  // start of chunk 0, absolute
   uint64_t n;
   uint8_t* ids;          // [n][32] (device)
   uint32_t* queue;       // chunk queue counter, zero at launch
   uint32_t nfirst;       // chunks handed out statically (one per lane of the grid)
   uint32_t pad;
+  uint64_t base_off;     // absolute position of blob[0]
+  // device-side range (the pipelined IndexFromFile, dsx_index.cpp): when
+  // range_lo is set, the chunks are ends[range_lo[0] .. range_hi[0]) with the
+  // first one starting at range_lo[1]; ids are written at the same indices.
+  // Records are {total cuts, carried cut} snapshots of the chain state.
+  const uint64_t* range_lo;
+  const uint64_t* range_hi;
 };
+
+// copies {DevState.total, DevState.carry} into rec[0..1] (the digest range
+// snapshot after a window's stitch)
+struct DevState;
+__global__ void state_snapshot_kernel(const DevState* st, uint64_t* rec);
 
 #ifndef DSX_DIGEST_THREADS
 #define DSX_DIGEST_THREADS 256

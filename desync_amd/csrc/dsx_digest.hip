@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "dsx_digest.h"
+#include "dsx_stitch.h"
 
 namespace dsx {
 
@@ -287,11 +288,32 @@ __device__ __forceinline__ void tail_block(const uint8_t* p, uint32_t r, bool ma
   }
 }
 
+__global__ void state_snapshot_kernel(const DevState* st, uint64_t* rec) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    rec[0] = st->total;
+    rec[1] = st->carry;
+  }
+}
+
 template <class H>
 __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
   constexpr int BLK = H::BLK;
   const uint32_t lane = threadIdx.x & 63u;
-  // chunk state
+  // chunk range: host-given, or device-side snapshots of the chain state
+  uint64_t n = a.n, first_start = a.first_start;
+  uint32_t nfirst = a.nfirst;
+  const uint64_t* ends = a.ends;
+  uint8_t* ids = a.ids;
+  if (a.range_lo) {
+    const uint64_t i0 = a.range_lo[0], i1 = a.range_hi[0];
+    n = i1 > i0 ? i1 - i0 : 0;
+    first_start = a.range_lo[1];
+    ends += i0;
+    ids += i0 * 32u;
+    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+    nfirst = (uint32_t)(n < lanes ? n : lanes);
+  }
+  // chunk state (s, e, pos relative to blob[0])
   uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // first chunk: static
   uint64_t s = 0, e = 0, pos = 0;
   uint32_t phase = 0;  // 0 = data blocks, 1 = tail with marker, 2 = length-only block
@@ -299,19 +321,26 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
   bool have_next = false;
   H st;
   auto start_chunk = [&]() {
-    if (ci < a.n) {
-      s = ci == 0 ? a.first_start : a.ends[ci - 1];
-      e = a.ends[ci];
-      pos = s;
-      phase = 0;
-      have_next = false;
-      st.init();
+    while (ci < n) {
+      const uint64_t sa = ci == 0 ? first_start : ends[ci - 1], ea = ends[ci];
+      // a chunk outside the readable bytes (malformed ends) is skipped and
+      // gets no ID instead of reading out of bounds
+      if (sa >= a.base_off && sa <= ea && ea - a.base_off <= a.len) {
+        s = sa - a.base_off;
+        e = ea - a.base_off;
+        pos = s;
+        phase = 0;
+        have_next = false;
+        st.init();
+        return;
+      }
+      ci = n;  // (this lane takes no further chunk)
     }
   };
-  if (ci >= a.nfirst) ci = a.n;  // (grid larger than the static share)
+  if (ci >= nfirst) ci = n;  // (grid larger than the static share)
   start_chunk();
   while (true) {
-    const bool live = ci < a.n;
+    const bool live = ci < n;
     if (__ballot(live) == 0) break;
     uint32_t d[32];
     bool finished = false;
@@ -347,7 +376,7 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
     }
     st.compress(d);  // (dead lanes compress garbage; their state is discarded)
     if (live && phase == 3) {
-      st.out(a.ids + ci * 32u);
+      st.out(ids + ci * 32u);
       finished = true;
     }
     // refill the finished lanes from the queue (one atomic per wave)
@@ -359,7 +388,7 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
       base = __shfl(base, __ffsll((long long)fm) - 1, 64);
       if (finished) {
         const uint32_t rank = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-        ci = (uint64_t)a.nfirst + base + rank;
+        ci = (uint64_t)nfirst + base + rank;
         start_chunk();
       }
     }

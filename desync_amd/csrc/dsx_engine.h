@@ -160,6 +160,19 @@ struct dsx_ctx {
   std::deque<Pending> pend;
   HostState* h_ring = nullptr;   // pinned, kQueueDepth slots
   HostState* h_cur = nullptr;    // slot the next enqueued piece publishes into
+
+  // IndexFromFile pipeline (dsx_index.cpp): pinned read slots, two HBM
+  // windows, chain-state snapshots that delimit each window's digest range
+  static constexpr int kIdxSlots = 8;
+  uint64_t index_window = 1ull << 30;  // DSX_INDEX_WINDOW: bytes per HBM window
+  uint64_t index_slot = 64ull << 20;   // DSX_INDEX_SLOT: bytes per pinned read slot
+  int index_readers = 4;               // DSX_INDEX_READERS: reader threads
+  uint8_t* idx_slots[kIdxSlots] = {};
+  uint64_t idx_slot_bytes = 0;
+  DevBuf<uint8_t> idx_win[2];
+  DevBuf<uint64_t> idx_snap;
+  hipEvent_t idx_copy_ev[kIdxSlots] = {};
+  hipEvent_t idx_win_ev[2] = {};
   hipEvent_t q_ev[kQueueDepth] = {};
   uint32_t q_next = 0;
 };
@@ -201,3 +214,5 @@ int read_state(dsx_ctx* c, HostState* out);
 int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_t halo,
                   uint64_t P, uint64_t len, bool is_last);
 int ensure_attr_walk(dsx_ctx* c);
+int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo);
+void index_release(dsx_ctx* c);  // dsx_index.cpp: frees the pipeline's buffers

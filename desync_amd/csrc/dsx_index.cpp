@@ -1,0 +1,329 @@
+// dsx_index.cpp -- IndexFromFile on the GPU: bytes from a file descriptor or
+// host memory -> cut list + chunk IDs (include/dsx.h: dsx_index_fd,
+// dsx_index_host).
+//
+// Reference: IndexFromFile (make.go:22-163) chunks the file with n goroutines
+// (split-and-align) and computes Digest.Sum of every chunk (make.go:223,
+// digest.go:11-29); GetFileSize (ioctl_linux.go:63-84) sizes regular files
+// and block devices.
+//
+// Pipeline (one context, two HIP streams, reader threads):
+//   reader threads  pread/memcpy 64 MiB pieces into a ring of pinned slots;
+//   copy_stream     H2D of each piece into the current HBM window;
+//   stream          scan + stitch (dsx_scan.hip, dsx_stitch.hip) every
+//                   256 MiB, the chain state carried on the device; at the
+//                   end of a window a snapshot of {total cuts, carried cut}
+//                   and digest_kernel over the chunks the window finished.
+// Two windows alternate, so the digest of window w overlaps the H2D and scan
+// of window w+1.  A window starts with the last max + 128 bytes of the
+// previous one: the carried cut lies in (P - max, P] (dsx_stitch.hip), so the
+// unfinished chunk and the scan's 48-byte warm-up are always in HBM.  No host
+// round trip happens until the end of the file.
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "dsx_engine.h"
+
+namespace {
+
+using FillFn = int (*)(void* ud, uint8_t* dst, uint64_t off, uint64_t n);
+
+// Reads pieces [k*piece, (k+1)*piece) of the source into slot k % K on
+// reader threads, ahead of the consumer, never more than K pieces ahead.
+class Prefetcher {
+ public:
+  Prefetcher(FillFn fill, void* ud, uint64_t len, uint64_t piece, uint8_t* const* slots, int nslots,
+             int nthreads)
+      : fill_(fill), ud_(ud), len_(len), piece_(piece), np_((len + piece - 1) / piece),
+        slots_(slots, slots + nslots), have_(nslots, -1), allow_(nslots), rc_(nslots, 0) {
+    for (int s = 0; s < nslots; ++s) allow_[s] = s;
+    const int nt = std::max(1, std::min<int>(nthreads, (int)std::min<uint64_t>(np_, 64)));
+    for (int i = 0; i < nt; ++i) th_.emplace_back([this] { run(); });
+  }
+  ~Prefetcher() { stop(); }
+  // blocks until piece k is in its slot; returns the fill status
+  int wait(uint64_t k, uint8_t** p, uint64_t* n) {
+    const size_t s = k % slots_.size();
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [&] { return have_[s] == (int64_t)k; });
+    *p = slots_[s];
+    *n = std::min(piece_, len_ - k * piece_);
+    return rc_[s];
+  }
+  // the slot holding piece k may be refilled (its H2D copy has landed)
+  void release(uint64_t k) {
+    const size_t s = k % slots_.size();
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      allow_[s] = (int64_t)(k + slots_.size());
+    }
+    cv_.notify_all();
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+    th_.clear();
+  }
+
+ private:
+  void run() {
+    while (true) {
+      uint64_t k;
+      size_t s;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        if (stop_ || next_ >= np_) return;
+        k = next_++;
+        s = k % slots_.size();
+        cv_.wait(lk, [&] { return stop_ || allow_[s] == (int64_t)k; });
+        if (stop_) return;
+      }
+      const uint64_t off = k * piece_;
+      const int rc = fill_(ud_, slots_[s], off, std::min(piece_, len_ - off));
+      {
+        std::lock_guard<std::mutex> lk(m_);
+        rc_[s] = rc;
+        have_[s] = (int64_t)k;
+      }
+      cv_.notify_all();
+    }
+  }
+  FillFn fill_;
+  void* ud_;
+  uint64_t len_, piece_, np_;
+  std::vector<uint8_t*> slots_;
+  std::vector<int64_t> have_, allow_;
+  std::vector<int> rc_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  uint64_t next_ = 0;
+  bool stop_ = false;
+  std::vector<std::thread> th_;
+};
+
+struct MemSrc {
+  const uint8_t* p;
+};
+int fill_mem(void* ud, uint8_t* dst, uint64_t off, uint64_t n) {
+  memcpy(dst, ((const MemSrc*)ud)->p + off, n);
+  return DSX_OK;
+}
+struct FdSrc {
+  int fd;
+  uint64_t base;
+};
+int fill_fd(void* ud, uint8_t* dst, uint64_t off, uint64_t n) {
+  const FdSrc* s = (const FdSrc*)ud;
+  uint64_t got = 0;
+  while (got < n) {
+    const ssize_t r = pread(s->fd, dst + got, n - got, (off_t)(s->base + off + got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return DSX_E_IO;
+    }
+    if (r == 0) return DSX_E_IO;  // the file shrank underneath us
+    got += (uint64_t)r;
+  }
+  return DSX_OK;
+}
+
+constexpr uint64_t kScanStep = 256ull << 20;  // bytes per scan + stitch launch
+
+int index_setup(dsx_ctx* c, uint64_t slot_bytes) {
+  if (c->idx_slot_bytes < slot_bytes) {
+    HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+    for (auto& s : c->idx_slots) {
+      if (s) (void)hipHostFree(s);
+      s = nullptr;
+    }
+    c->idx_slot_bytes = 0;
+    for (auto& s : c->idx_slots) HIPCHK(c, hipHostMalloc((void**)&s, slot_bytes));
+    c->idx_slot_bytes = slot_bytes;
+  }
+  for (auto& e : c->idx_copy_ev)
+    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : c->idx_win_ev)
+    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return DSX_OK;
+}
+
+// Drains both streams (after an error or a cancel: nothing may still read the
+// pinned slots or the windows when the call returns).
+int drain(dsx_ctx* c, Prefetcher& pf, int rc) {
+  pf.stop();
+  (void)hipStreamSynchronize(c->copy_stream);
+  (void)hipStreamSynchronize(c->stream);
+  return rc;
+}
+
+int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
+              uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {
+  HIPCHK(c, hipSetDevice(c->device));
+  c->err.clear();
+  int rc = ensure_attr_walk(c);
+  if (rc) return rc;
+  *n_out = 0;
+  if (len == 0) return DSX_OK;  // empty file: no chunks (TestChunkerEmptyFile)
+  const uint64_t need = len / p->min + 2;
+  // geometry: pieces (pinned slots) tile the windows exactly; a window keeps
+  // `pre` bytes of its predecessor in front (>= max + 64, line aligned)
+  const uint64_t pre = (p->max + 64 + kLine - 1) / kLine * kLine;
+  uint64_t piece = std::min<uint64_t>(c->index_slot, std::max<uint64_t>(len, 4096));
+  piece = (piece + 4095) & ~4095ull;
+  uint64_t W = std::max<uint64_t>(c->index_window, 2 * pre);
+  W = (W + piece - 1) / piece * piece;
+  if (W >= len) W = (len + piece - 1) / piece * piece;  // one window
+  const uint64_t nwin = (len + W - 1) / W;
+  const uint64_t scan_step = std::max<uint64_t>(piece, kScanStep / piece * piece);
+  rc = index_setup(c, piece);
+  if (rc) return rc;
+  HIPCHK(c, grow(c, c->idx_win[0], pre + W));
+  if (nwin > 1) HIPCHK(c, grow(c, c->idx_win[1], pre + W));
+  HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 1)));
+  HIPCHK(c, grow(c, c->out, need));
+  HIPCHK(c, grow(c, c->dg_ids, need * 32));
+  const int K = dsx_ctx::kIdxSlots;
+
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    CallCfg cc{p, len, 0, kRound, c->out.p, need, attempt == 1};
+    rc = reset_state(c, 0);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->idx_snap.p, 0, 2 * sizeof(uint64_t), c->stream));  // {0 cuts, cut 0}
+    Prefetcher pf(fill, ud, len, piece, c->idx_slots, K, c->index_readers);
+    uint64_t k = 0;  // piece index
+    for (uint64_t w = 0; w < nwin; ++w) {
+      const uint64_t ws = w * W, wl = std::min(W, len - ws);
+      uint8_t* buf = c->idx_win[w & 1].p;
+      // the digest of window w-2 read this buffer; the copy stream waits for it
+      if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
+      if (w >= 1)  // the previous window's last `pre` bytes (it was a full window)
+        HIPCHK(c, hipMemcpyAsync(buf, c->idx_win[(w - 1) & 1].p + W, pre,
+                                 hipMemcpyDeviceToDevice, c->copy_stream));
+      uint64_t scanned = ws;
+      for (uint64_t off = ws; off < ws + wl; off += piece, ++k) {
+        if (c->cancel.load()) return drain(c, pf, DSX_E_INTERRUPTED);
+        uint8_t* hp = nullptr;
+        uint64_t hn = 0;
+        rc = pf.wait(k, &hp, &hn);
+        if (rc) return drain(c, pf, rc);
+        hipError_t e = hipMemcpyAsync(buf + pre + (off - ws), hp, hn, hipMemcpyHostToDevice,
+                                      c->copy_stream);
+        if (e == hipSuccess) e = hipEventRecord(c->idx_copy_ev[k % K], c->copy_stream);
+        // keep two copies queued: the previous slot returns to the readers
+        // once its copy has landed
+        if (e == hipSuccess && k >= 1) e = hipEventSynchronize(c->idx_copy_ev[(k - 1) % K]);
+        if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: H2D"));
+        if (k >= 1) pf.release(k - 1);
+        const uint64_t end = off + hn;
+        if (end == ws + wl || end - scanned >= scan_step) {
+          e = hipStreamWaitEvent(c->stream, c->idx_copy_ev[k % K], 0);
+          if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: wait"));
+          const uint64_t halo = w == 0 ? scanned : pre + (scanned - ws);
+          rc = enqueue_piece(c, cc, buf + pre + (scanned - ws), halo, scanned, end - scanned,
+                             end == len);
+          if (rc) return drain(c, pf, rc);
+          scanned = end;
+        }
+      }
+      // the window's finished chunks: [snap[w].total, snap[w+1].total) from
+      // snap[w].carry, all inside this window's bytes
+      hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
+                         (const DevState*)c->state.p, c->idx_snap.p + 2 * (w + 1));
+      DigestArgs da{};
+      da.blob = w == 0 ? buf + pre : buf;
+      da.base_off = w == 0 ? 0 : ws - pre;
+      da.len = w == 0 ? wl : pre + wl;
+      da.ends = c->out.p;
+      da.ids = c->dg_ids.p;
+      da.range_lo = c->idx_snap.p + 2 * w;
+      da.range_hi = c->idx_snap.p + 2 * (w + 1);
+      rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
+      if (rc) return drain(c, pf, rc);
+      hipError_t e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
+      if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
+    }
+    pf.stop();
+    HostState st;
+    rc = read_state(c, &st);  // waits for the last digest too (same stream)
+    HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+    if (rc) return rc;
+    if (st.err & kErrDense) {  // rare: a lane overflowed its candidate slots
+      c->stats.dense_fallbacks++;
+      continue;
+    }
+    if (st.err) {
+      c->err = "index: stitch error";
+      return DSX_E_INTERNAL;
+    }
+    c->stats.chunks = st.total;
+    *n_out = st.total;
+    if (st.total > cap) return DSX_E_CAPACITY;
+    if (st.total) {
+      HIPCHK(c, hipMemcpy(out_ends, c->out.p, st.total * 8, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(out_ids, c->dg_ids.p, st.total * 32, hipMemcpyDeviceToHost));
+    }
+    return DSX_OK;
+  }
+  c->err = "dense-candidate path overflowed";
+  return DSX_E_INTERNAL;
+}
+
+}  // namespace
+
+void index_release(dsx_ctx* c) {
+  for (auto& s : c->idx_slots) {
+    if (s) (void)hipHostFree(s);
+    s = nullptr;
+  }
+  c->idx_slot_bytes = 0;
+  c->idx_win[0].release();
+  c->idx_win[1].release();
+  c->idx_snap.release();
+  for (auto& e : c->idx_copy_ev)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
+  for (auto& e : c->idx_win_ev)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
+}
+
+static bool bad_algo(int algo) { return algo != DSX_DIGEST_SHA512_256 && algo != DSX_DIGEST_SHA256; }
+
+extern "C" int dsx_index_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, const dsx_params_t* p,
+                            int algo, uint64_t* out_ends, uint8_t* ids, uint64_t cap,
+                            uint64_t* n_out) {
+  if (!c || !p || !n_out || fd < 0 || (cap && (!out_ends || !ids)) || bad_algo(algo))
+    return DSX_E_INVAL;
+  if (len == UINT64_MAX) {
+    // GetFileSize (ioctl_linux.go:63-84): lseek(SEEK_END) gives the size of
+    // a regular file and of a block device alike
+    const off_t end = lseek(fd, 0, SEEK_END);
+    if (end < 0) return DSX_E_IO;
+    len = (uint64_t)end > off ? (uint64_t)end - off : 0;
+  }
+  FdSrc s{fd, off};
+  const int rc = run_index(c, p, algo, len, fill_fd, &s, out_ends, ids, cap, n_out);
+  c->cancel.store(0);  // a dsx_cancel() issued before or during this call ends here
+  return rc;
+}
+
+extern "C" int dsx_index_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, const dsx_params_t* p,
+                              int algo, uint64_t* out_ends, uint8_t* ids, uint64_t cap,
+                              uint64_t* n_out) {
+  if (!c || !p || !n_out || (len && !h_blob) || (cap && (!out_ends || !ids)) || bad_algo(algo))
+    return DSX_E_INVAL;
+  MemSrc s{(const uint8_t*)h_blob};
+  const int rc = run_index(c, p, algo, len, fill_mem, &s, out_ends, ids, cap, n_out);
+  c->cancel.store(0);
+  return rc;
+}

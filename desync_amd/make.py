@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+import stat as _stat
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -78,7 +80,7 @@ def cut_fd(fd, min_size, avg_size, max_size, offset=0, length=None, ctx=None):
     p = Params(min_size, avg_size, max_size)
     ctx = ctx or _lib.default_context()
     if length is None:
-        length = os.fstat(fd).st_size - offset
+        length = max(0, file_size(fd) - offset)
     out, cap = _ends_buffer(length, min_size)
     n = ctypes.c_uint64()
     check(lib().dsx_cut_fd(ctx.h, fd, offset, length, ctypes.byref(p.c), out.ctypes.data, cap,
@@ -137,13 +139,18 @@ def chunk_ids(ptr, length, ends, start=0, ctx=None, algo=None):
 _PIECE = 64 << 20   # bytes per pinned staging slot
 _SLOTS = 4          # slots in flight (reads of one overlap the H2D of the others)
 _staging = {}       # device -> list of pinned host tensors, reused across calls
+_staging_lock = threading.Lock()
 
 
 def _file_to_device(f, size, device):
-    """The whole file in HBM (288 GB per MI355X).  Pieces of 64 MiB are read
-    with os.preadv by a small thread pool (the GIL is released) into a ring of
-    pinned slots and copied to the device asynchronously on a side stream, so
-    page-cache reads and the PCIe transfer overlap."""
+    """The whole file in HBM (288 GB per MI355X), for VerifyIndex.  Pieces of
+    64 MiB are read with os.preadv by a small thread pool (the GIL is
+    released) into a ring of pinned slots and copied to the device
+    asynchronously on a side stream, so page-cache reads and the PCIe transfer
+    overlap.  The pinned slots are shared per device under a lock; the side
+    stream first waits for the current stream (the caching allocator may hand
+    back memory that queued work still uses), and is drained before the slots
+    or the tensor are released, also when a read fails."""
     import concurrent.futures as cf
 
     import torch
@@ -151,55 +158,169 @@ def _file_to_device(f, size, device):
     t = torch.empty(max(size, 1), dtype=torch.uint8, device=dev)
     if size == 0:
         return t
-    slots = _staging.get(device)
-    if slots is None:
-        slots = [torch.empty(_PIECE, dtype=torch.uint8).pin_memory() for _ in range(_SLOTS)]
-        _staging[device] = slots
     fd = f.fileno()
-    stream = torch.cuda.Stream(device=dev)
-    done = [None] * _SLOTS  # event of the last H2D out of each slot
     npieces = (size + _PIECE - 1) // _PIECE
+    with _staging_lock:
+        slots = _staging.get(device)
+        if slots is None:
+            slots = [torch.empty(_PIECE, dtype=torch.uint8).pin_memory() for _ in range(_SLOTS)]
+            _staging[device] = slots
 
-    def read(k):
-        off = k * _PIECE
-        n = min(_PIECE, size - off)
-        mv = memoryview(slots[k % _SLOTS].numpy())[:n]
-        got = 0
-        while got < n:
-            r = os.preadv(fd, [mv[got:]], off + got)
-            if r <= 0:
-                raise OSError(f"short read at offset {off + got}")
-            got += r
-        return n
+        def read(k):
+            off = k * _PIECE
+            n = min(_PIECE, size - off)
+            mv = memoryview(slots[k % _SLOTS].numpy())[:n]
+            got = 0
+            while got < n:
+                r = os.preadv(fd, [mv[got:]], off + got)
+                if r <= 0:
+                    raise OSError(f"short read at offset {off + got}")
+                got += r
+            return n
 
-    with cf.ThreadPoolExecutor(max_workers=_SLOTS) as pool:
-        futs = {}
-        for k in range(min(_SLOTS, npieces)):
-            futs[k] = pool.submit(read, k)
-        for k in range(npieces):
-            n = futs.pop(k).result()
-            slot = k % _SLOTS
-            with torch.cuda.stream(stream):
-                t[k * _PIECE:k * _PIECE + n].copy_(slots[slot][:n], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(stream)
-            done[slot] = ev
-            nxt = k + _SLOTS
-            if nxt < npieces:
-                ev.synchronize()  # the slot is free once its copy has landed
-                futs[nxt] = pool.submit(read, nxt)
-    stream.synchronize()
+        stream = torch.cuda.Stream(device=dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        try:
+            with cf.ThreadPoolExecutor(max_workers=_SLOTS) as pool:
+                futs = {k: pool.submit(read, k) for k in range(min(_SLOTS, npieces))}
+                try:
+                    for k in range(npieces):
+                        n = futs.pop(k).result()
+                        with torch.cuda.stream(stream):
+                            t[k * _PIECE:k * _PIECE + n].copy_(slots[k % _SLOTS][:n],
+                                                              non_blocking=True)
+                            ev = torch.cuda.Event()
+                            ev.record(stream)
+                        if k + _SLOTS < npieces:
+                            ev.synchronize()  # the slot is free once its copy has landed
+                            futs[k + _SLOTS] = pool.submit(read, k + _SLOTS)
+                finally:
+                    for fu in futs.values():  # (an error: let pending reads finish)
+                        fu.cancel()
+        finally:
+            stream.synchronize()
+        torch.cuda.current_stream(dev).wait_stream(stream)
     return t
+
+
+def file_size(fd):
+    """GetFileSize (ioctl_linux.go:63-84): st_size for regular files, the
+    BLKGETSIZE64 ioctl for block devices (whose st_size is 0)."""
+    st = os.fstat(fd)
+    if _stat.S_ISBLK(st.st_mode):
+        import fcntl
+        import struct
+        BLKGETSIZE64 = 0x80081272
+        return struct.unpack("Q", fcntl.ioctl(fd, BLKGETSIZE64, b"\0" * 8))[0]
+    return st.st_size
+
+
+def _digest_code(algo=None):
+    if algo is None:
+        algo = digest.Digest.Algorithm()
+    if algo in ("sha512-256", _lib.DSX_DIGEST_SHA512_256):
+        return _lib.DSX_DIGEST_SHA512_256
+    if algo in ("sha256", _lib.DSX_DIGEST_SHA256):
+        return _lib.DSX_DIGEST_SHA256
+    raise ValueError(f"unknown digest {algo!r}")
+
+
+class _CancelWatch:
+    """Polls a Go-style ctx (``done()``) during a long library call and turns
+    it into dsx_cancel (make.go:201-203 -> Interrupted)."""
+
+    def __init__(self, ctx, dctx):
+        import threading
+        self.ctx, self.dctx = ctx, dctx
+        self.stop = threading.Event()
+        self.t = None
+        if ctx is not None and hasattr(ctx, "done"):
+            self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self.stop.wait(0.02):
+            if self.ctx.done():
+                lib().dsx_cancel(self.dctx.h)
+                return
+
+    def __enter__(self):
+        if self.t:
+            self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        if self.t:
+            self.t.join()
+        return False
+
+
+def index_fd(fd, min_size, avg_size, max_size, offset=0, length=None, algo=None, ctx=None,
+             device=0, cancel=None):
+    """dsx_index_fd: a file range -> (chunk end offsets relative to ``offset``,
+    uint8 array of 32-byte chunk IDs), both computed on the GPU.  ``length``
+    None means to the end (files and block devices)."""
+    p = Params(min_size, avg_size, max_size)
+    code = _digest_code(algo)
+    size = length if length is not None else max(0, file_size(fd) - offset)
+    cap = size // min_size + 2
+    ends = np.empty(cap, dtype=np.uint64)
+    ids = np.empty((cap, 32), dtype=np.uint8)
+    n = ctypes.c_uint64()
+
+    def call(c):
+        with _CancelWatch(cancel, c):
+            rc = lib().dsx_index_fd(c.h, fd, offset, size, ctypes.byref(p.c), code,
+                                    ends.ctypes.data, ids.ctypes.data, cap, ctypes.byref(n))
+        if rc == _lib.DSX_E_INTERRUPTED:
+            raise Interrupted()
+        check(rc, c.h)
+
+    if ctx is not None:
+        call(ctx)
+    else:
+        with _lib.pooled_context(device) as c:
+            call(c)
+    return ends[:n.value].copy(), ids[:n.value].copy()
+
+
+def index_host(data, min_size, avg_size, max_size, algo=None, ctx=None, device=0):
+    """dsx_index_host: a host-memory blob -> (chunk ends, chunk IDs) on the GPU."""
+    p = Params(min_size, avg_size, max_size)
+    code = _digest_code(algo)
+    arr = np.ascontiguousarray(np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+                               if not isinstance(data, np.ndarray) else data, dtype=np.uint8)
+    cap = arr.size // min_size + 2
+    ends = np.empty(cap, dtype=np.uint64)
+    ids = np.empty((cap, 32), dtype=np.uint8)
+    n = ctypes.c_uint64()
+    with (_lib.pooled_context(device) if ctx is None else _nullctx(ctx)) as c:
+        check(lib().dsx_index_host(c.h, arr.ctypes.data, arr.size, ctypes.byref(p.c), code,
+                                   ends.ctypes.data, ids.ctypes.data, cap, ctypes.byref(n)), c.h)
+    return ends[:n.value].copy(), ids[:n.value].copy()
+
+
+class _nullctx:
+    def __init__(self, v):
+        self.v = v
+
+    def __enter__(self):
+        return self.v
+
+    def __exit__(self, *exc):
+        return False
 
 
 def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0):
     """make.go:22-163 -- chunk a file into an Index (not stored anywhere).
 
-    The file is read into HBM once; the cut list (dsx_cut_device) and the
-    chunk IDs (dsx_chunk_ids) are computed there.  ``n`` (the reference's
-    worker count) has no effect on the result, as in the reference.  ``ctx``
-    mirrors the Go context: any object with a ``done()`` method (or None);
-    when it reports done, Interrupted is raised (make.go:201-203).
+    One library call (dsx_index_fd) does the data path: reader threads stream
+    the file (or block device) through pinned memory into HBM, where the cut
+    list (scan + stitch) and the chunk IDs (Digest.Sum, SHA-512/256 or SHA-256)
+    are computed.  ``n`` (the reference's worker count) has no effect on the
+    result, as in the reference.  ``ctx`` mirrors the Go context: any object
+    with a ``done()`` method (or None); when it reports done the call stops
+    between 64 MiB pieces and Interrupted is raised (make.go:201-203).
     """
     pb = pb or NullProgressBar()
     stats = ChunkingStats()
@@ -211,23 +332,17 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
     with open(name, "rb") as f:
         head = f.read(64)
         index.Index.FeatureFlags |= catar_feature_flags(head)  # make.go:49-61
-        size = os.fstat(f.fileno()).st_size  # GetFileSize, make.go:64
-        f.seek(0)
+        size = file_size(f.fileno())  # GetFileSize, make.go:64
         pb.SetTotal(size)
         pb.Start()
         try:
             if ctx is not None and getattr(ctx, "done", lambda: False)():
                 raise Interrupted()
-            dctx = _lib.default_context(device)
-            blob = _file_to_device(f, size, device)
-            ends = cut_device(blob.data_ptr(), size, min_size, avg_size, max_size, ctx=dctx)
-            if ctx is not None and getattr(ctx, "done", lambda: False)():
-                raise Interrupted()
-            ids = chunk_ids(blob.data_ptr(), size, ends, 0, ctx=dctx)
-            del blob
+            ends, ids = index_fd(f.fileno(), min_size, avg_size, max_size, 0, size,
+                                 device=device, cancel=ctx)
             starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64) if ends.size else ends
             for s, e, cid in zip(starts.tolist(), ends.tolist(), ids):
-                index.Chunks.append(IndexChunk(ID=cid, Start=s, Size=e - s))
+                index.Chunks.append(IndexChunk(ID=cid.tobytes(), Start=s, Size=e - s))
                 pb.Set(e)
             stats.ChunksAccepted = len(index.Chunks)
             stats.ChunksProduced = len(index.Chunks)

@@ -232,6 +232,25 @@ int dsx_gen_dedup(dsx_ctx_t *ctx, void *d_dst, uint64_t offset, uint64_t len, ui
 int dsx_chunk_ids(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, uint64_t start,
                   const uint64_t *ends, uint64_t n, void *ids, uint32_t flags, int algo);
 
+/* ---- IndexFromFile on the GPU: cut list + chunk IDs ----------------------------
+ * The whole of IndexFromFile's data path (make.go:22-163: chunking, then
+ * Digest.Sum of every chunk, make.go:223) for a file descriptor range
+ * [off, off+len) or a host-memory blob.  len == UINT64_MAX (fd only) means
+ * "to the end", for regular files and block devices alike (GetFileSize,
+ * ioctl_linux.go:63-84).  Reader threads pread into pinned staging, the bytes
+ * are copied to HBM while the next ones are read, chunked there, and hashed
+ * there (algo: DSX_DIGEST_*); files larger than the HBM window
+ * (DSX_INDEX_WINDOW, 1 GiB) stream through two alternating windows.  The fd's
+ * file offset is not used or changed.
+ * out_ends: chunk END offsets relative to off (cap entries); ids: 32 bytes per
+ * chunk (cap * 32 bytes); both host memory.  DSX_E_CAPACITY sets *n_out to the
+ * required count (len/min + 2 always suffices).  Synchronous; dsx_cancel()
+ * interrupts it between 64 MiB pieces (DSX_E_INTERRUPTED). */
+int dsx_index_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, const dsx_params_t *p,
+                 int algo, uint64_t *out_ends, uint8_t *ids, uint64_t cap, uint64_t *n_out);
+int dsx_index_host(dsx_ctx_t *ctx, const void *h_blob, uint64_t len, const dsx_params_t *p,
+                   int algo, uint64_t *out_ends, uint8_t *ids, uint64_t cap, uint64_t *n_out);
+
 /* ---- statistics (ChunkingStats, make.go:329-341 + scan/stitch timings) ------ */
 typedef struct dsx_stats {
     uint64_t chunks;            /* ChunksAccepted */

@@ -1,0 +1,162 @@
+"""dsx_index_fd / dsx_index_host: IndexFromFile's whole data path (file or
+host blob -> cut list + chunk IDs) on the GPU, against the oracle.
+
+Reference: IndexFromFile (make.go:22-163, IDs at make.go:223), flags
+(make.go:35-62), GetFileSize (ioctl_linux.go:63-84), Interrupted
+(make.go:201-203), TestChunkerEmptyFile (chunker_test.go:69-80) for the
+empty file's 104-byte caibx.
+"""
+import ctypes
+import hashlib
+import io
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle as o
+
+pytestmark = pytest.mark.gpu
+
+MIN, AVG, MAX = 16 * 1024, 64 * 1024, 256 * 1024
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _ids(buf, ends, algo="sha512-256"):
+    raw = buf.tobytes() if isinstance(buf, np.ndarray) else buf
+    name = "sha512_256" if algo == "sha512-256" else "sha256"
+    out, s = [], 0
+    for e in ends.tolist():
+        out.append(hashlib.new(name, raw[s:e]).digest())
+        s = e
+    return out
+
+
+def test_abi_probe_without_torch():
+    """A pure C-ABI caller (tests/abi_index_probe.py: ctypes + struct, no
+    torch) reproduces the four golden caibx files byte for byte through
+    dsx_index_fd."""
+    r = subprocess.run([sys.executable, os.path.join(HERE, "abi_index_probe.py")],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("ok ") == 4 and "torch imported: False" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
+@pytest.mark.parametrize("kind", ["uniform", "nulls", "small-params"])
+def test_index_fd_many_windows(tmp_path, monkeypatch, algo, kind):
+    """1 MiB HBM windows and 256 KiB read slots: dozens of windows, chunks
+    carried across every window boundary, zero runs across them."""
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_INDEX_WINDOW", str(1 << 20))
+    monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 18))
+    params = (MIN, AVG, MAX) if kind != "small-params" else (1024, 4096, 16384)
+    if kind == "nulls":
+        r = o.synth_uniform(41, 0, 4 * MAX + 999)
+        data = np.concatenate([r, np.zeros(10 * MAX + 77, np.uint8), r, np.zeros(3 * MAX, np.uint8), r])
+    else:
+        data = o.synth_uniform(40, 0, (40 << 20) + 333)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ctx = _lib.Context(0)
+    try:
+        fd = os.open(str(f), os.O_RDONLY)
+        try:
+            ends, ids = desync_amd.index_fd(fd, *params, algo=algo, ctx=ctx)
+        finally:
+            os.close(fd)
+    finally:
+        ctx.close()
+    ref = o.chunk_stream(data, *params)
+    assert np.array_equal(ends, ref)
+    assert [bytes(x) for x in ids] == _ids(data, ref, algo)
+
+
+def test_index_host_two_gib_windows():
+    """1.5 GiB through the default 1 GiB windows (two of them): every cut
+    against oracle.chunk_parallel, every ID against hashlib."""
+    import concurrent.futures as cf
+
+    import desync_amd
+    n = (3 << 29) + 777
+    data = o.synth_uniform_c(17, 0, n)
+    ends, ids = desync_amd.index_host(data, MIN, AVG, MAX)
+    ref = o.chunk_parallel(data, MIN, AVG, MAX, o.default_threads())
+    assert np.array_equal(ends, ref)
+    starts = np.concatenate([[0], ref[:-1]]).astype(np.uint64)
+    mv = memoryview(data)
+
+    def h(i):
+        return hashlib.new("sha512_256", mv[int(starts[i]):int(ref[i])]).digest()
+
+    with cf.ThreadPoolExecutor(o.default_threads()) as pool:
+        want = list(pool.map(h, range(ref.size), chunksize=256))
+    assert [bytes(x) for x in ids] == want
+
+
+def test_empty_file_and_sha256_flags(tmp_path, golden):
+    """The empty file gives the 104-byte caibx (header + table marker + tail);
+    under --digest sha256 the index flags lack CaFormatSHA512256
+    (make.go:35-38) and the IDs are SHA-256."""
+    import desync_amd
+    from desync_amd import digest
+    f = tmp_path / "empty"
+    f.write_bytes(b"")
+    index, stats = desync_amd.IndexFromFile(None, str(f), 4, MIN, AVG, MAX)
+    b = io.BytesIO()
+    index.WriteTo(b)
+    assert len(b.getvalue()) == 104 and stats.ChunksAccepted == 0
+    assert b.getvalue() == o.encode_caibx(o.index_flags(b""), MIN, AVG, MAX, [], [])
+    g = tmp_path / "blob1"
+    g.write_bytes(golden("blob1"))
+    ref = o.decode_caibx(golden("blob1.caibx"))
+    prev = digest.Digest.Algorithm()
+    desync_amd.set_digest("sha256")
+    try:
+        index, _ = desync_amd.IndexFromFile(None, str(g), 4, ref["min"], ref["avg"], ref["max"])
+    finally:
+        desync_amd.set_digest(prev)
+    assert index.Index.FeatureFlags == o.CA_FORMAT_EXCLUDE_NO_DUMP
+    data = np.frombuffer(golden("blob1"), np.uint8)
+    assert [c.Start + c.Size for c in index.Chunks] == ref["ends"].tolist()
+    assert [c.ID for c in index.Chunks] == _ids(data, ref["ends"], "sha256")
+
+
+def test_index_cancel_and_io_error(tmp_path):
+    """dsx_cancel before the call -> Interrupted (and the next call runs);
+    a range past the end of the file -> DSX_E_IO."""
+    import desync_amd
+    from desync_amd import _lib
+    data = o.synth_uniform(42, 0, 5 << 20)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ctx = _lib.Context(0)
+    fd = os.open(str(f), os.O_RDONLY)
+    try:
+        _lib.lib().dsx_cancel(ctx.h)
+        with pytest.raises(desync_amd.Interrupted):
+            desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+        ends, _ = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+        assert np.array_equal(ends, o.chunk_stream(data, MIN, AVG, MAX))
+        with pytest.raises(_lib.DsxError) as ei:
+            desync_amd.index_fd(fd, MIN, AVG, MAX, length=data.size + 4096, ctx=ctx)
+        assert ei.value.code == _lib.DSX_E_IO
+    finally:
+        os.close(fd)
+        ctx.close()
+
+
+def test_chunk_ids_rejects_malformed_ends(dctx):
+    """host ends are validated (order, bounds) before any launch."""
+    import torch
+    from desync_amd import _lib
+    t = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    out = np.empty((3, 32), np.uint8)
+    for ends, start in (([100, 50, 4096], 0), ([100, 200, 5000], 0), ([100, 200, 300], 150)):
+        e = np.array(ends, np.uint64)
+        rc = _lib.lib().dsx_chunk_ids(dctx.h, ctypes.c_void_p(t.data_ptr()), 4096, start,
+                                      e.ctypes.data, 3, out.ctypes.data, 0, 0)
+        assert rc == _lib.DSX_E_INVAL, ends

@@ -45,6 +45,13 @@ def main():
             b = io.BytesIO()
             index.WriteTo(b)
             dt = time.perf_counter() - t0
+            fdr = os.open(path, os.O_RDONLY)
+            try:
+                t1 = time.perf_counter()
+                ends, _ = desync_amd.index_fd(fdr, MIN, AVG, MAX)
+                dt_c = time.perf_counter() - t1
+            finally:
+                os.close(fdr)
             raw = np.fromfile(path, dtype=np.uint8)
             want = desync_amd.cut_host(raw, MIN, AVG, MAX)
             got = np.array([c.Start + c.Size for c in index.Chunks], dtype=np.uint64)
@@ -54,11 +61,12 @@ def main():
                 assert hashlib.new("sha512_256", piece).digest() == c.ID
             del raw
             rows.append({"gib": gib, "chunks": stats.ChunksAccepted, "caibx_bytes": len(b.getvalue()),
-                         "s": round(dt, 4), "gibs": round(gib / dt, 2)})
+                         "s": round(dt, 4), "gibs": round(gib / dt, 2),
+                         "index_fd_s": round(dt_c, 4), "index_fd_gibs": round(gib / dt_c, 2)})
         finally:
             os.unlink(path)
     print(json.dumps({"tool": "make_rate", "params": "16/64/256 KiB", "digest": "sha512-256",
-                      "rows": rows, "note": "page-cache file -> HBM -> cuts + IDs -> caibx bytes"}))
+                      "rows": rows, "note": "page-cache file -> HBM -> cuts + IDs -> caibx bytes (IndexFromFile); index_fd = the C call alone (dsx_index_fd)"}))
 
 
 if __name__ == "__main__":
