@@ -13,7 +13,7 @@ mirror of the reference's Go API for that path:
 
 There is no CPU fallback: without libdsx.so or a GPU, calls raise.
 """
-from .chunker import ChunkerWindowSize, Chunker, NewChunker, Params  # noqa: F401
+from .chunker import ChunkerReadError, ChunkerWindowSize, Chunker, NewChunker, Params  # noqa: F401
 from .digest import SHA256, SHA512256, NewNullChunk, NullChunk, set_digest  # noqa: F401
 from .errors import Interrupted  # noqa: F401
 from .index import FormatIndex, Index, IndexChunk, IndexFromReader  # noqa: F401
@@ -21,7 +21,7 @@ from .make import ChunkingStats, IndexFromFile, VerifyError, VerifyIndex, chunk_
     cut_fd, cut_host, file_size, index_fd, index_host  # noqa: F401
 
 __all__ = [
-    "ChunkerWindowSize", "Chunker", "NewChunker", "Params", "SHA256", "SHA512256", "NullChunk",
+    "ChunkerWindowSize", "Chunker", "ChunkerReadError", "NewChunker", "Params", "SHA256", "SHA512256", "NullChunk",
     "NewNullChunk", "set_digest", "Interrupted", "FormatIndex", "Index", "IndexChunk",
     "IndexFromReader", "ChunkingStats", "IndexFromFile", "cut_device", "cut_device_result",
     "cut_fd", "cut_host", "chunk_ids", "VerifyIndex", "VerifyError", "file_size", "index_fd",

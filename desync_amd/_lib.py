@@ -36,6 +36,8 @@ DSX_E_IO = -11
 DSX_E_STATE = -12
 DSX_E_INTERNAL = -13
 DSX_E_RESYNC = -14
+DSX_STREAM_EOF = 1
+DSX_STREAM_SYNC = 2
 DSX_SEAM_DEVICE = 8
 DSX_SEAM_LAST = 1
 DSX_SEAM_REWALKED = 2
@@ -45,7 +47,8 @@ EXPORTS = (
     "dsx_params_init", "dsx_strerror", "dsx_abi_version", "dsx_ctx_create", "dsx_ctx_destroy",
     "dsx_last_error", "dsx_cancel", "dsx_cut_device", "dsx_sync", "dsx_result", "dsx_cut_host",
     "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
-    "dsx_stream_done", "dsx_stream_end", "dsx_stream_chunk_data", "dsx_shard_local", "dsx_shard_resolve",
+    "dsx_stream_done", "dsx_stream_end", "dsx_stream_chunk_data", "dsx_stream_buffer",
+    "dsx_stream_commit", "dsx_stream_flush", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host",
 )
@@ -137,6 +140,9 @@ def lib():
             "dsx_stream_advance": (i32, [vp, u64]),
             "dsx_stream_done": (i32, [vp]),
             "dsx_stream_end": (i32, [vp]),
+            "dsx_stream_buffer": (i32, [vp, u64, P(vp)]),
+            "dsx_stream_commit": (i32, [vp, u64, i32]),
+            "dsx_stream_flush": (i32, [vp, P(u64), P(u64)]),
             "dsx_stream_chunk_data": (vp, [vp]),
             "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), vp, u32]),
             "dsx_shard_resolve": (i32, [vp, vp, i32, i32, vp, vp, u64, P(u64), u32]),

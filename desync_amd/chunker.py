@@ -9,10 +9,16 @@ Reference interface (chunker.go):
 
 Same argument meaning and error behaviour: NewChunker validates in the
 reference order and raises ValueError with the reference's message; Next()
-returns (start, b'') at the end of the stream; read errors propagate.
+returns (start, b'') at the end of the stream; the returned chunk is a
+read-only view of library memory, valid until the next call (Next's rule,
+chunker.go:202-205: copy it to keep it).  A reader error surfaces where the
+reference's would: Next() raises ChunkerReadError carrying (start, chunk,
+cause), the chunk being all bytes buffered after start (split(n, err),
+chunker.go:207-211), and chunking starts over behind them.
+
 The boundary scan and cut chain run on the GPU (libdsx.so); this class only
-moves bytes from the reader into the library (dsx_stream_push) and hands
-out confirmed chunks (dsx_stream_pop).
+moves bytes from the reader into the library (straight into its pinned
+buffer with readinto when the reader has it) and hands out confirmed chunks.
 """
 from __future__ import annotations
 
@@ -22,8 +28,8 @@ from . import _lib
 from ._lib import check, lib
 
 ChunkerWindowSize = 48
-# reads per refill; the reference refills 10*max (chunker.go:179)
-_READ_FACTOR = 10
+# bytes per reader call: the library sends 32 MiB batches to the GPU
+_READ = 16 << 20
 
 
 class Params:
@@ -43,8 +49,27 @@ class Params:
         return int(self.c.discriminator)
 
 
+class ChunkerReadError(IOError):
+    """Next()'s (start, b, err) with err != nil: ``start`` and ``chunk`` (the
+    buffered bytes, chunker.go:207-211) and the reader's exception as
+    ``__cause__``."""
+
+    def __init__(self, start, chunk, cause):
+        super().__init__(f"read error after stream position {start + len(chunk)}: {cause!r}")
+        self.start = start
+        self.chunk = chunk
+        self.__cause__ = cause
+
+
+def _view(ptr, n):
+    if n == 0:
+        return memoryview(b"")
+    return memoryview((ctypes.c_ubyte * n).from_address(ptr)).cast("B").toreadonly()
+
+
 class Chunker:
-    """Content-defined chunker over a file-like reader (``read(n) -> bytes``)."""
+    """Content-defined chunker over a file-like reader (``readinto(buf)`` or
+    ``read(n)``)."""
 
     def __init__(self, reader, min_size, avg_size, max_size, ctx=None, device=0):
         self.params = Params(min_size, avg_size, max_size)
@@ -59,25 +84,51 @@ class Chunker:
         self._eof = False
         self._start = ctypes.c_uint64()
         self._size = ctypes.c_uint64()
+        self._ptr = ctypes.c_void_p()
+        # the reference's buffer bookkeeping, replayed to place reader errors
+        # exactly: Next() refills when fewer than max bytes are buffered
+        # (chunker.go:207) and reads up to 10*max (chunker.go:179)
+        self._cur = 0       # start of the next chunk
+        self._R = 0         # end of the reference's buffer
+        self._pos = 0       # bytes received from the reader
+        self._err = None    # pending reader exception ...
+        self._E = 0         # ... raised at stream position _E
+        self._synced = False
 
     # -- reference API -----------------------------------------------------
     def Next(self):
-        """(start, chunk bytes); (start, b'') when the stream is exhausted."""
+        """(start, chunk view); (start, empty) when the stream is exhausted."""
         L = lib()
         h = self.ctx.h
+        mx = self.params.max
+        if self._R - self._cur < mx:  # the reference's fillBuffer
+            target = self._cur + 10 * mx
+            while self._pos < target and not self._eof and self._err is None:
+                self._fill()  # (our reads run ahead of the reference's; make sure they do)
+            if self._err is not None and target > self._E:
+                return self._read_error()
+            self._R = target
         while True:
             rc = check(L.dsx_stream_pop(h, ctypes.byref(self._start), ctypes.byref(self._size)), h)
             if rc == 1:
-                ptr = L.dsx_stream_chunk_data(h)
                 n = self._size.value
-                return self._start.value, ctypes.string_at(ptr, n)
+                self._cur = self._start.value + n
+                return self._start.value, _view(L.dsx_stream_chunk_data(h), n)
             if self._eof:
-                return self._start.value, b""
+                return self._start.value, memoryview(b"")
+            if self._err is not None:
+                if self._synced:  # cannot happen: the next chunk ends before _E
+                    raise RuntimeError("stream stalled behind a reader error")
+                check(L.dsx_stream_commit(h, 0, _lib.DSX_STREAM_SYNC), h)
+                self._synced = True
+                continue
             self._fill()
 
     def Advance(self, n):
         """Skip n bytes and restart the hash as if the stream began there."""
         check(lib().dsx_stream_advance(self.ctx.h, int(n)), self.ctx.h)
+        self._cur += int(n)
+        self._R = max(self._R, self._cur)
 
     def Min(self):
         return self.params.min
@@ -114,18 +165,38 @@ class Chunker:
             yield start, b
 
     # -- internals -------------------------------------------------------------
+    def _read_error(self):
+        L, h = lib(), self.ctx.h
+        check(L.dsx_stream_flush(h, ctypes.byref(self._start), ctypes.byref(self._size)), h)
+        start, n = self._start.value, self._size.value
+        chunk = bytes(_view(L.dsx_stream_chunk_data(h), n))
+        err, self._err, self._synced = self._err, None, False
+        self._cur = self._R = start + n
+        raise ChunkerReadError(start, chunk, err)
+
     def _fill(self):
-        want = _READ_FACTOR * self.params.max
-        data = self.r.read(want)  # reader errors propagate (chunker.go:208-211)
-        if not data:
-            self._eof = True
-            check(lib().dsx_stream_push(self.ctx.h, None, 0, 1), self.ctx.h)
+        L, h = lib(), self.ctx.h
+        check(L.dsx_stream_buffer(h, _READ, ctypes.byref(self._ptr)), h)
+        try:
+            if hasattr(self.r, "readinto"):
+                got = self.r.readinto(_writable(self._ptr.value, _READ))
+            else:
+                data = self.r.read(_READ)
+                got = len(data) if data else 0
+                if got:
+                    ctypes.memmove(self._ptr.value, data, got)
+        except Exception as e:  # noqa: BLE001 -- any reader failure is Next's err
+            self._err, self._E = e, self._pos
             return
-        if not isinstance(data, bytes):
-            data = bytes(data)
-        # bytes are immutable and stay alive for the call: passed without a copy
-        # (the library copies what it keeps, dsx.h)
-        check(lib().dsx_stream_push(self.ctx.h, data, len(data), 0), self.ctx.h)
+        got = got or 0
+        self._pos += got
+        if got == 0:
+            self._eof = True
+        check(L.dsx_stream_commit(h, got, _lib.DSX_STREAM_EOF if got == 0 else 0), h)
+
+
+def _writable(ptr, n):
+    return memoryview((ctypes.c_ubyte * n).from_address(ptr)).cast("B")
 
 
 def NewChunker(reader, min_size, avg_size, max_size, **kw):

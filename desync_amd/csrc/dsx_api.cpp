@@ -222,6 +222,7 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   if (c->h_res) (void)hipHostFree(c->h_res);
   c->dbuf[0].release(); c->dbuf[1].release();
   index_release(c);
+  stream_release(c);
   for (auto& p : c->pinned) if (p) (void)hipHostFree(p);
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
@@ -812,176 +813,6 @@ extern "C" int dsx_cut_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, cons
   }
   FdSrc s{fd, off};
   return run_host_pipeline(c, p, len, fill_fd, &s, out_ends, cap, n_out);
-}
-
-// --------------------------------------------------------------------------
-// streaming: Chunker.Next / Advance over an io.Reader (chunker.go:206-309)
-// --------------------------------------------------------------------------
-extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
-  if (!c || !p) return DSX_E_INVAL;
-  // one stream per context (its scratch and carried state live here): a
-  // second Chunker on a context whose stream is still being read is refused
-  // instead of silently resetting the first one
-  if (c->st.active && !(c->st.done && c->st.cuts.empty())) {
-    c->err = "a stream is already active on this context (dsx_stream_end it first)";
-    return DSX_E_STATE;
-  }
-  c->st = dsx_ctx::Stream();
-  c->st.active = true;
-  c->st.p = *p;
-  return ensure_attr_walk(c);
-}
-
-// Scan everything pushed so far (one piece) and append the confirmed cuts.
-static int stream_process(dsx_ctx* c) {
-  auto& s = c->st;
-  const uint64_t buf_end = s.buf_pos + s.buf.size();
-  if (buf_end <= s.scan_pos && !(s.eof && !s.done)) return DSX_OK;
-  HIPCHK(c, hipSetDevice(c->device));
-  const uint64_t len = buf_end - s.scan_pos;
-  if (len == 0 && s.eof) {
-    // end of input exactly at the scanned position: finish the chain
-    if (s.carry < buf_end) {
-      // successor of carry is the tail (len - carry <= max here, no candidates left)
-      s.cuts.push_back(buf_end);
-      s.carry = buf_end;
-    }
-    s.done = true;
-    return DSX_OK;
-  }
-  // bytes kept before scan_pos (never before the chain origin: those are
-  // virtual zeros for the scan)
-  const uint64_t halo = std::min<uint64_t>(64, s.scan_pos - std::max(s.buf_pos, s.origin));
-  HIPCHK(c, grow(c, c->dbuf[0], len + 64));
-  HIPCHK(c, hipMemcpyAsync(c->dbuf[0].p, s.buf.data() + (s.scan_pos - halo - s.buf_pos),
-                           len + halo, hipMemcpyHostToDevice, c->stream));
-  const uint64_t need = (buf_end - s.carry) / s.p.min + 4;
-  HIPCHK(c, grow(c, c->out, need));
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    CallCfg cc{&s.p, buf_end, s.origin, s.origin + kRound, c->out.p, need, attempt == 1};
-    int rc = reset_state(c, s.carry);
-    if (rc) return rc;
-    if (!cc.dense) {
-      rc = enqueue_piece(c, cc, c->dbuf[0].p + halo, halo, s.scan_pos, len, s.eof);
-      if (rc) return rc;
-    } else {
-      for (uint64_t o = 0; o < len; o += kDensePiece) {
-        const uint64_t n = std::min(kDensePiece, len - o);
-        rc = enqueue_piece(c, cc, c->dbuf[0].p + halo + o, halo + o, s.scan_pos + o, n,
-                           s.eof && o + n == len);
-        if (rc) return rc;
-      }
-    }
-    HostState st;
-    rc = read_state(c, &st);
-    if (rc) return rc;
-    if (st.err & kErrDense) {
-      c->stats.dense_fallbacks++;
-      continue;
-    }
-    if (st.err) {
-      c->err = "stream: stitch error";
-      return DSX_E_INTERNAL;
-    }
-    if (st.total) {
-      std::vector<uint64_t> v(st.total);
-      HIPCHK(c, hipMemcpy(v.data(), c->out.p, st.total * 8, hipMemcpyDeviceToHost));
-      for (uint64_t x : v) s.cuts.push_back(x);
-    }
-    s.carry = st.carry;
-    s.scan_pos = buf_end;
-    if (s.eof) s.done = true;
-    return DSX_OK;
-  }
-  c->err = "dense-candidate path overflowed";
-  return DSX_E_INTERNAL;
-}
-
-extern "C" int dsx_stream_push(dsx_ctx_t* c, const void* bytes, uint64_t len, int eof) {
-  if (!c || (len && !bytes)) return DSX_E_INVAL;
-  auto& s = c->st;
-  if (!s.active || s.eof) return DSX_E_STATE;
-  const uint8_t* b = (const uint8_t*)bytes;
-  if (s.skip) {  // Advance() beyond the buffered bytes drops future input
-    const uint64_t d = std::min(s.skip, len);
-    s.skip -= d;
-    b += d;
-    len -= d;
-  }
-  // compact: keep bytes from min(cur, scan_pos - 64)
-  uint64_t keep_from = std::min(s.cur, s.scan_pos >= 64 ? s.scan_pos - 64 : 0);
-  keep_from = std::max(keep_from, s.buf_pos);
-  // Drop consumed bytes only once they are at least half the buffer: each
-  // byte is moved O(1) times instead of once per push.
-  if (keep_from > s.buf_pos && 2 * (keep_from - s.buf_pos) >= s.buf.size()) {
-    s.buf.erase(s.buf.begin(), s.buf.begin() + (keep_from - s.buf_pos));
-    s.buf_pos = keep_from;
-  }
-  s.last_chunk = nullptr;
-  s.buf.insert(s.buf.end(), b, b + len);
-  if (eof) s.eof = true;
-  const uint64_t pending = s.buf_pos + s.buf.size() - s.scan_pos;
-  if (pending >= kStreamBatch || s.eof) return stream_process(c);
-  return DSX_OK;
-}
-
-extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
-  if (!c || !start || !size) return DSX_E_INVAL;
-  auto& s = c->st;
-  if (!s.active) return DSX_E_STATE;
-  if (s.cuts.empty()) {
-    *start = s.cur;
-    *size = 0;
-    return 0;
-  }
-  const uint64_t e = s.cuts.front();
-  s.cuts.pop_front();
-  *start = s.cur;
-  *size = e - s.cur;
-  s.last_chunk = s.buf.data() + (s.cur - s.buf_pos);
-  s.cur = e;
-  return 1;
-}
-
-extern "C" const uint8_t* dsx_stream_chunk_data(dsx_ctx_t* c) { return c ? c->st.last_chunk : nullptr; }
-
-extern "C" int dsx_stream_end(dsx_ctx_t* c) {
-  if (!c) return DSX_E_INVAL;
-  c->st = dsx_ctx::Stream();
-  return DSX_OK;
-}
-
-extern "C" int dsx_stream_done(dsx_ctx_t* c) {
-  if (!c) return 0;
-  return c->st.active && c->st.done && c->st.cuts.empty() ? 1 : 0;
-}
-
-extern "C" int dsx_stream_advance(dsx_ctx_t* c, uint64_t n) {
-  if (!c) return DSX_E_INVAL;
-  auto& s = c->st;
-  if (!s.active) return DSX_E_STATE;
-  const uint64_t target = s.cur + n;
-  const uint64_t buf_end = s.buf_pos + s.buf.size();
-  s.cuts.clear();
-  s.last_chunk = nullptr;
-  if (target <= buf_end) {
-    s.buf.erase(s.buf.begin(), s.buf.begin() + (target - s.buf_pos));
-    s.skip = 0;
-  } else {
-    s.buf.clear();
-    s.skip = target - buf_end;
-  }
-  s.buf_pos = target;
-  s.scan_pos = target;
-  s.origin = target;
-  s.cur = target;
-  s.carry = target;
-  s.done = false;
-  if (s.eof) {
-    s.skip = 0;
-    return stream_process(c);  // remaining buffered bytes form the rest of the stream
-  }
-  return DSX_OK;
 }
 
 // --------------------------------------------------------------------------

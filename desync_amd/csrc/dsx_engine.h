@@ -120,12 +120,36 @@ struct dsx_ctx {
 
   // streaming state (Chunker.Next over an io.Reader)
   struct Stream {
-    bool active = false, eof = false, done = false;
+    static constexpr int kSlots = 3;  // batches on the GPU at once
+    struct Batch {
+      uint64_t P, len, seq;
+      bool last;
+      int slot;
+    };
+    bool active = false, eof = false, done = false, final_pending = false;
+    bool fresh = true;   // the next batch starts the chain at fresh_carry
+    bool dense = false;  // dense-candidate mode (after a lane overflow)
     dsx_params_t p{};
-    std::vector<uint8_t> buf;
-    uint64_t buf_pos = 0, scan_pos = 0, origin = 0, cur = 0, skip = 0, carry = 0;
-    std::deque<uint64_t> cuts;
+    uint64_t batch = 32ull << 20;  // DSX_STREAM_BATCH: bytes per device batch
+    uint8_t* h = nullptr;          // pinned host buffer: stream bytes [hbase, hend)
+    uint64_t hcap = 0, hbase = 0, hend = 0;
+    uint64_t cur = 0;     // consumer position (start of the next chunk)
+    uint64_t origin = 0;  // chain origin (0, an Advance target, a read-error restart)
+    uint64_t sched = 0;   // bytes before this have been handed to the GPU
+    uint64_t carry = 0;   // chain position after the collected batches
+    uint64_t fresh_carry = 0;
+    uint64_t skip = 0;    // Advance past the held bytes: future bytes to drop
+    std::deque<uint64_t> cuts;  // confirmed chunk ends not yet popped
+    std::deque<Batch> fly;      // batches on the GPU, oldest first
+    int next_slot = 0;
     const uint8_t* last_chunk = nullptr;
+    // per-slot resources
+    DevBuf<uint8_t> dbuf[kSlots];
+    DevBuf<uint64_t> dout[kSlots];
+    uint64_t* hcut[kSlots] = {};
+    uint64_t hcut_cap[kSlots] = {};
+    HostState* hstate = nullptr;  // pinned, kSlots entries
+    hipEvent_t copy_ev[kSlots] = {}, done_ev[kSlots] = {};
   } st;
 
   // multi-GPU shard state (dsx_shard_local -> dsx_shard_resolve)
@@ -215,4 +239,5 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
                   uint64_t P, uint64_t len, bool is_last);
 int ensure_attr_walk(dsx_ctx* c);
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo);
-void index_release(dsx_ctx* c);  // dsx_index.cpp: frees the pipeline's buffers
+void index_release(dsx_ctx* c);   // dsx_index.cpp: frees the pipeline's buffers
+void stream_release(dsx_ctx* c);  // dsx_stream.cpp: frees the stream's buffers

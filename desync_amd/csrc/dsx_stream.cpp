@@ -1,0 +1,413 @@
+// dsx_stream.cpp -- Chunker.Next / Advance over an io.Reader
+// (chunker.go:175-309; the stdin / pipe path of `desync tar -i`,
+// cmd/desync/tar.go:140, and `desync chunk`, cmd/desync/chunk.go:63).
+//
+// The reader's bytes land in a pinned host buffer (dsx_stream_buffer hands
+// out the write pointer, so a reader can fill it directly; dsx_stream_push
+// copies).  Every `batch` bytes (32 MiB) the library enqueues, without
+// waiting: H2D of the batch on the copy stream, then scan + stitch on the
+// compute stream with the chain state carried on the device, then D2H of the
+// batch's cuts into pinned memory.  Up to three batches are on the GPU while
+// the reader fills the next one; dsx_stream_pop collects a batch only when
+// its cuts are needed and no more input can be taken first.  A chunk is
+// confirmed once the bytes up to its start + max are scanned, as in the
+// reference where Next() needs len(buf) >= max (chunker.go:207, 221).
+// Popped chunk bytes alias the host buffer until the next call (Next's rule,
+// chunker.go:202-205).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "dsx_engine.h"
+
+namespace {
+
+using Stream = dsx_ctx::Stream;
+constexpr int kSlots = Stream::kSlots;
+constexpr uint64_t kHalo = 64;  // bytes re-sent before a batch (the scan's 48-byte warm-up)
+
+int st_setup(dsx_ctx* c) {
+  auto& s = c->st;
+  if (!s.hstate) HIPCHK(c, hipHostMalloc((void**)&s.hstate, kSlots * sizeof(HostState)));
+  for (int i = 0; i < kSlots; ++i) {
+    if (!s.copy_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&s.copy_ev[i], hipEventDisableTiming));
+    if (!s.done_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&s.done_ev[i], hipEventDisableTiming));
+  }
+  return DSX_OK;
+}
+
+// Waits for every batch on the GPU and forgets their results.
+int st_drain(dsx_ctx* c) {
+  auto& s = c->st;
+  HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  s.fly.clear();
+  return DSX_OK;
+}
+
+// Room for `want` more bytes at the tail of the host buffer.  Bytes below
+// keep_from are dropped: nothing needs them (the consumer is past them, and
+// every batch that could still be re-sent starts after them).
+int st_room(dsx_ctx* c, uint64_t want) {
+  auto& s = c->st;
+  if (s.h && s.hend - s.hbase + want <= s.hcap) return DSX_OK;
+  uint64_t keep = std::min(s.cur, s.sched >= kHalo ? s.sched - kHalo : 0);
+  if (!s.fly.empty()) keep = std::min(keep, s.fly.front().P >= kHalo ? s.fly.front().P - kHalo : 0);
+  keep = std::max(keep, s.hbase);
+  const uint64_t held = s.hend - keep;
+  // queued H2D copies read the buffer: they must have landed before it moves
+  for (const auto& b : s.fly) HIPCHK(c, hipEventSynchronize(s.copy_ev[b.slot]));
+  if (held + want <= s.hcap && keep > s.hbase) {
+    memmove(s.h, s.h + (keep - s.hbase), held);
+    s.hbase = keep;
+    return DSX_OK;
+  }
+  uint64_t ncap = std::max<uint64_t>(s.hcap ? s.hcap : 4 * s.batch, 4 * s.batch);
+  while (ncap < held + want) ncap *= 2;
+  uint8_t* n = nullptr;
+  HIPCHK(c, hipHostMalloc((void**)&n, ncap));
+  if (held) memcpy(n, s.h + (keep - s.hbase), held);
+  if (s.h) (void)hipHostFree(s.h);
+  s.h = n;
+  s.hcap = ncap;
+  s.hbase = keep;
+  return DSX_OK;
+}
+
+// Enqueue the next batch [sched, sched + len) (last: it ends the stream).
+int st_collect(dsx_ctx* c);
+int st_issue(dsx_ctx* c, uint64_t len, bool last) {
+  auto& s = c->st;
+  if ((int)s.fly.size() >= kSlots) return st_collect(c);  // st_pump comes back (its sched may move)
+  const int slot = s.next_slot;
+  s.next_slot = (slot + 1) % kSlots;
+  const uint64_t P = s.sched;
+  const uint64_t halo = std::min<uint64_t>(kHalo, P - std::max(s.hbase, s.origin));
+  const uint64_t bound = len / s.p.min + 4;
+  HIPCHK(c, grow(c, s.dbuf[slot], halo + len + 64));
+  HIPCHK(c, grow(c, s.dout[slot], bound));
+  if (s.hcut_cap[slot] < bound) {
+    if (s.hcut[slot]) (void)hipHostFree(s.hcut[slot]);
+    s.hcut[slot] = nullptr;
+    s.hcut_cap[slot] = 0;
+    const uint64_t cap = bound + bound / 4 + 64;
+    HIPCHK(c, hipHostMalloc((void**)&s.hcut[slot], cap * sizeof(uint64_t)));
+    s.hcut_cap[slot] = cap;
+  }
+  HIPCHK(c, hipMemcpyAsync(s.dbuf[slot].p, s.h + (P - halo - s.hbase), halo + len,
+                           hipMemcpyHostToDevice, c->copy_stream));
+  HIPCHK(c, hipEventRecord(s.copy_ev[slot], c->copy_stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, s.copy_ev[slot], 0));
+  if (s.fresh) {
+    int rc = reset_state(c, s.fresh_carry);  // the scan initialises the chain state
+    if (rc) return rc;
+    s.fresh = false;
+  } else {
+    // the chain carries on; the batch's cuts start at out[0]
+    HIPCHK(c, hipMemsetAsync(&c->state.p->total, 0, sizeof(uint64_t), c->stream));
+    c->npiece_call = 0;
+  }
+  CallCfg cc{&s.p, P + len, s.origin, s.origin + kRound, s.dout[slot].p, bound, s.dense};
+  c->h_cur = &s.hstate[slot];
+  int rc = DSX_OK;
+  if (!s.dense) {
+    rc = enqueue_piece(c, cc, s.dbuf[slot].p + halo, halo, P, len, last);
+  } else {
+    for (uint64_t o = 0; o < len && !rc; o += kDensePiece) {
+      const uint64_t n = std::min(kDensePiece, len - o);
+      rc = enqueue_piece(c, cc, s.dbuf[slot].p + halo + o, halo + o, P + o, n, last && o + n == len);
+    }
+  }
+  c->h_cur = c->h_state;
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(s.hcut[slot], s.dout[slot].p, bound * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipEventRecord(s.done_ev[slot], c->stream));
+  s.fly.push_back({P, len, c->piece_seq, last, slot});
+  s.sched = P + len;
+  return DSX_OK;
+}
+
+// Collect the oldest batch: its cuts join the queue.
+int st_collect(dsx_ctx* c) {
+  auto& s = c->st;
+  const Stream::Batch b = s.fly.front();
+  HIPCHK(c, hipEventSynchronize(s.done_ev[b.slot]));
+  HostState hs;
+  memcpy(&hs, (const void*)&s.hstate[b.slot], sizeof hs);
+  if (hs.seq != b.seq) {
+    c->err = "stream: stale batch state";
+    return DSX_E_INTERNAL;
+  }
+  if (hs.err & kErrDense) {
+    // rare: a scan lane overflowed its candidate slots.  Every batch after
+    // this one ran on a wrong chain; redo from this batch on the dense path
+    // (its bytes are still held: st_room keeps the oldest batch's bytes)
+    int rc = st_drain(c);
+    if (rc) return rc;
+    c->stats.dense_fallbacks++;
+    s.dense = true;
+    s.fresh = true;
+    s.fresh_carry = s.carry;
+    s.sched = b.P;
+    return DSX_OK;  // the caller re-issues (st_pump)
+  }
+  if (hs.err) {
+    c->err = "stream: stitch error";
+    return DSX_E_INTERNAL;
+  }
+  for (uint64_t i = 0; i < hs.total; ++i) s.cuts.push_back(s.hcut[b.slot][i]);
+  s.carry = hs.carry;
+  if (b.last) s.done = true;
+  s.fly.pop_front();
+  c->stats.chunks += hs.total;
+  return DSX_OK;
+}
+
+// Hand the held bytes to the GPU in batches (all of them at the end of the
+// stream or on a sync).
+int st_pump(dsx_ctx* c, bool sync) {
+  auto& s = c->st;
+  while (true) {
+    const uint64_t avail = s.hend - s.sched;
+    int rc = DSX_OK;
+    if (avail > s.batch || (avail == s.batch && !s.eof)) {
+      rc = st_issue(c, s.batch, false);
+    } else if (s.eof) {
+      if (avail > 0) {
+        rc = st_issue(c, avail, true);
+      } else {
+        if (!s.done && (s.fly.empty() || !s.fly.back().last)) s.final_pending = true;
+        return DSX_OK;
+      }
+    } else if (sync && avail > 0) {
+      rc = st_issue(c, avail, false);
+    } else {
+      return DSX_OK;
+    }
+    if (rc) return rc;
+  }
+}
+
+// End of stream exactly at the last scanned byte: the chain's last chunk
+// ends there (no candidate after the carried cut, or it would have been
+// emitted: dsx_stitch.hip's undetermined-successor rule).
+void st_finish(dsx_ctx* c) {
+  auto& s = c->st;
+  if (s.carry < s.hend) {
+    s.cuts.push_back(s.hend);
+    s.carry = s.hend;
+  }
+  s.final_pending = false;
+  s.done = true;
+}
+
+void st_restart(dsx_ctx* c, uint64_t at) {
+  auto& s = c->st;
+  s.cuts.clear();
+  s.origin = s.sched = s.carry = s.fresh_carry = at;
+  s.fresh = true;
+  s.done = s.final_pending = false;
+}
+
+}  // namespace
+
+void stream_release(dsx_ctx* c) {
+  auto& s = c->st;
+  if (s.h) (void)hipHostFree(s.h);
+  s.h = nullptr;
+  for (int i = 0; i < kSlots; ++i) {
+    s.dbuf[i].release();
+    s.dout[i].release();
+    if (s.hcut[i]) (void)hipHostFree(s.hcut[i]);
+    s.hcut[i] = nullptr;
+    if (s.copy_ev[i]) (void)hipEventDestroy(s.copy_ev[i]);
+    if (s.done_ev[i]) (void)hipEventDestroy(s.done_ev[i]);
+    s.copy_ev[i] = s.done_ev[i] = nullptr;
+  }
+  if (s.hstate) (void)hipHostFree(s.hstate);
+  s.hstate = nullptr;
+}
+
+extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
+  if (!c || !p) return DSX_E_INVAL;
+  auto& s = c->st;
+  // one stream per context (its scratch and carried state live here): a
+  // second Chunker on a context whose stream is still being read is refused
+  // instead of silently resetting the first one
+  if (s.active && !(s.done && s.cuts.empty())) {
+    c->err = "a stream is already active on this context (dsx_stream_end it first)";
+    return DSX_E_STATE;
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = ensure_attr_walk(c);
+  if (!rc) rc = st_setup(c);
+  if (!rc) rc = st_drain(c);
+  if (rc) return rc;
+  s.active = true;
+  s.eof = false;
+  s.dense = false;
+  s.p = *p;
+  if (const char* v = getenv("DSX_STREAM_BATCH"))
+    s.batch = std::max<uint64_t>(4096, (uint64_t)atoll(v));
+  s.hbase = s.hend = s.cur = s.skip = 0;
+  s.next_slot = 0;
+  s.last_chunk = nullptr;
+  st_restart(c, 0);
+  c->stats.chunks = 0;
+  return DSX_OK;
+}
+
+extern "C" int dsx_stream_end(dsx_ctx_t* c) {
+  if (!c) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (s.active) {
+    (void)hipSetDevice(c->device);
+    int rc = st_drain(c);
+    if (rc) return rc;
+  }
+  s.active = s.eof = false;
+  st_restart(c, 0);
+  s.done = false;
+  s.last_chunk = nullptr;
+  return DSX_OK;
+}
+
+extern "C" int dsx_stream_buffer(dsx_ctx_t* c, uint64_t want, uint8_t** ptr) {
+  if (!c || !ptr) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active || s.eof) return DSX_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  s.last_chunk = nullptr;
+  int rc = st_room(c, want);
+  if (rc) return rc;
+  *ptr = s.h + (s.hend - s.hbase);
+  return DSX_OK;
+}
+
+extern "C" int dsx_stream_commit(dsx_ctx_t* c, uint64_t n, int flags) {
+  if (!c) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active || s.eof) return DSX_E_STATE;
+  if (n && (!s.h || s.hend - s.hbase + n > s.hcap)) return DSX_E_INVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  s.last_chunk = nullptr;
+  if (s.skip && n) {  // Advance() beyond the held bytes drops future input
+    uint8_t* tail = s.h + (s.hend - s.hbase);
+    const uint64_t d = std::min(s.skip, n);
+    s.skip -= d;
+    n -= d;
+    if (n) memmove(tail, tail + d, n);
+  }
+  s.hend += n;
+  if (flags & DSX_STREAM_EOF) s.eof = true;
+  const bool sync = (flags & DSX_STREAM_SYNC) != 0;
+  int rc = st_pump(c, sync);
+  // SYNC: no more input for now (the reader failed): everything held is
+  // scanned and collected, so pop returns every chunk it can confirm
+  while (!rc && sync && !s.fly.empty()) {
+    rc = st_collect(c);
+    if (!rc) rc = st_pump(c, true);
+  }
+  return rc;
+}
+
+extern "C" int dsx_stream_push(dsx_ctx_t* c, const void* bytes, uint64_t len, int eof) {
+  if (!c || (len && !bytes)) return DSX_E_INVAL;
+  uint8_t* dst = nullptr;
+  int rc = dsx_stream_buffer(c, len, &dst);
+  if (rc) return rc;
+  if (len) memcpy(dst, bytes, len);
+  return dsx_stream_commit(c, len, eof ? DSX_STREAM_EOF : 0);
+}
+
+extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
+  if (!c || !start || !size) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active) return DSX_E_STATE;
+  while (s.cuts.empty()) {
+    if (!s.fly.empty()) {
+      // collect now if the oldest batch is finished, if no more input can
+      // come, or if enough batches are queued; otherwise ask for input
+      // first, so the reader works while the GPU does
+      const bool ready = hipEventQuery(s.done_ev[s.fly.front().slot]) == hipSuccess;
+      if (!(ready || s.eof || s.fly.size() >= 2)) break;
+      HIPCHK(c, hipSetDevice(c->device));
+      int rc = st_collect(c);
+      if (!rc) rc = st_pump(c, false);  // (re-issues after a dense redo)
+      if (rc) return rc;
+      continue;
+    }
+    if (s.final_pending) {
+      st_finish(c);
+      continue;
+    }
+    break;
+  }
+  if (s.cuts.empty()) {
+    *start = s.cur;
+    *size = 0;
+    return 0;
+  }
+  const uint64_t e = s.cuts.front();
+  s.cuts.pop_front();
+  *start = s.cur;
+  *size = e - s.cur;
+  s.last_chunk = s.h + (s.cur - s.hbase);
+  s.cur = e;
+  return 1;
+}
+
+extern "C" const uint8_t* dsx_stream_chunk_data(dsx_ctx_t* c) { return c ? c->st.last_chunk : nullptr; }
+
+extern "C" int dsx_stream_done(dsx_ctx_t* c) {
+  if (!c) return 0;
+  const auto& s = c->st;
+  return s.active && s.done && s.cuts.empty() ? 1 : 0;
+}
+
+extern "C" int dsx_stream_flush(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
+  if (!c || !start || !size) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active) return DSX_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = st_drain(c);
+  if (rc) return rc;
+  // Next()'s read-error path (chunker.go:207-211 -> split(n, err)): every
+  // held byte after the consumer position is one chunk, and chunking starts
+  // over behind it
+  *start = s.cur;
+  *size = s.hend - s.cur;
+  s.last_chunk = s.h ? s.h + (s.cur - s.hbase) : nullptr;
+  s.cur = s.hend;
+  st_restart(c, s.hend);
+  s.eof = false;
+  return DSX_OK;
+}
+
+extern "C" int dsx_stream_advance(dsx_ctx_t* c, uint64_t n) {
+  if (!c) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active) return DSX_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = st_drain(c);
+  if (rc) return rc;
+  // Advance (chunker.go:292-309): the held bytes count first, then the
+  // reader's; the chunker behaves as if the stream started at cur + n
+  const uint64_t target = s.cur + n;
+  s.last_chunk = nullptr;
+  if (target <= s.hend) {
+    s.skip = 0;
+  } else {
+    s.skip = target - s.hend;
+    s.hbase = s.hend = target;  // nothing held
+  }
+  s.cur = target;
+  st_restart(c, target);
+  if (s.eof) {
+    s.skip = 0;
+    return st_pump(c, false);  // the remaining held bytes are the rest of the stream
+  }
+  return DSX_OK;
+}

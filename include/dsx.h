@@ -122,28 +122,45 @@ int dsx_cut_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, const dsx_par
 /* ---- streaming (Chunker.Next / Advance over an io.Reader) -------------------
  * One stream per context (a Chunker owns its context, as each Go Chunker owns
  * its buffer and hash state, chunker.go:108-131).
- * begin: starts a stream at position 0 with params p (NewChunker).  Returns
- *        DSX_E_STATE while another stream on ctx is unfinished.
- * end:   drops the stream state (the context can begin a new one).
- * push:  appends bytes read from the reader; eof=1 marks the end of input.
- *        The library copies the bytes (caller keeps ownership).
- * pop:   start and size of the next confirmed chunk.  Returns 1 if a chunk was
- *        produced, 0 if more input is needed (or the stream ended: then
- *        dsx_stream_done() is 1), or a negative error.
+ * begin:  starts a stream at position 0 with params p (NewChunker).  Returns
+ *         DSX_E_STATE while another stream on ctx is unfinished.
+ * end:    drops the stream (the context can begin a new one).
+ * buffer: room for `want` bytes at the tail of the library's pinned host
+ *         buffer; *ptr is where the caller writes them (e.g. the reader
+ *         reads straight into it).  Valid until the next call on ctx.
+ * commit: the caller wrote n bytes at *ptr.  flags: DSX_STREAM_EOF marks the
+ *         end of input; DSX_STREAM_SYNC means no more input is coming for
+ *         now (a failed reader): everything held is scanned and collected.
+ *         Full 32 MiB batches are sent to the GPU without waiting (H2D +
+ *         scan + stitch, up to 3 batches in flight).
+ * push:   buffer + memcpy + commit (eof != 0: DSX_STREAM_EOF).
+ * pop:    start and size of the next confirmed chunk.  Returns 1 if a chunk
+ *         was produced, 0 if more input is needed first (or the stream
+ *         ended: then dsx_stream_done() is 1), or a negative error.  Blocks
+ *         on the GPU only when its result is needed and no input can be
+ *         taken first.
+ * chunk_data: the bytes of the chunk returned by the last pop or flush (host
+ *         memory, valid until the next call on ctx -- Next()'s aliasing
+ *         rule, chunker.go:202-205).
+ * flush:  Next()'s read-error path (chunker.go:207-211, split(n, err)): all
+ *         held bytes after the consumer position as one chunk; chunking then
+ *         starts over behind them.
  * advance: Chunker.Advance(n) (chunker.go:292-309): drop n bytes at the
- *        current position (buffered first, then future pushes), reset the
- *        hash state, and continue as if the stream started there.
- * Chunk boundaries only depend on bytes in (start+min-48, start+max], so
- * a chunk is confirmed as soon as those bytes have been pushed. */
+ *         current position (held bytes first, then future input), and
+ *         continue as if the stream started there.
+ * A chunk is confirmed once the bytes up to its start + max are scanned, as
+ * Next() needs len(buf) >= max (chunker.go:207, 221). */
+#define DSX_STREAM_EOF 1
+#define DSX_STREAM_SYNC 2
 int dsx_stream_begin(dsx_ctx_t *ctx, const dsx_params_t *p);
+int dsx_stream_end(dsx_ctx_t *ctx);
+int dsx_stream_buffer(dsx_ctx_t *ctx, uint64_t want, uint8_t **ptr);
+int dsx_stream_commit(dsx_ctx_t *ctx, uint64_t n, int flags);
 int dsx_stream_push(dsx_ctx_t *ctx, const void *bytes, uint64_t len, int eof);
 int dsx_stream_pop(dsx_ctx_t *ctx, uint64_t *start, uint64_t *size);
+int dsx_stream_flush(dsx_ctx_t *ctx, uint64_t *start, uint64_t *size);
 int dsx_stream_advance(dsx_ctx_t *ctx, uint64_t n);
 int dsx_stream_done(dsx_ctx_t *ctx);
-int dsx_stream_end(dsx_ctx_t *ctx);
-/* Pointer to the bytes of the chunk returned by the last pop (host memory,
- * valid until the next push/pop/advance -- Next()'s aliasing rule,
- * chunker.go:202-205). */
 const uint8_t *dsx_stream_chunk_data(dsx_ctx_t *ctx);
 
 /* ---- multi-GPU shards (split-and-align across ranks) ------------------------

@@ -319,6 +319,79 @@ def test_stream_matches(dctx):
     assert ends == ref.tolist()
 
 
+class _FailingReader:
+    """Serves data[:E], raises OSError once, then serves data[E:] (resume) or
+    nothing (EOF)."""
+
+    def __init__(self, data, E, resume, chunk=3 << 20):
+        self.b, self.E, self.resume, self.pos, self.failed, self.chunk = data, E, resume, 0, False, chunk
+
+    def read(self, n):
+        if not self.failed and self.pos >= self.E:
+            self.failed = True
+            raise OSError("injected read error")
+        if not self.failed:
+            limit = self.E
+        else:
+            limit = len(self.b) if self.resume else self.pos  # resume, or EOF
+        end = min(self.pos + n, self.pos + self.chunk, limit)
+        out = self.b[self.pos:end]
+        self.pos = end
+        return out
+
+
+def _go_next_with_error(data, E, resume, mn, av, mx):
+    """What the reference's Chunker.Next returns (chunker.go:175-277) when the
+    reader fails at stream position E: chunks of the sequential chain while
+    its buffer holds >= max bytes, then (cur, data[cur:E], err) at the first
+    fillBuffer that would cross E, then chunking starts over at E."""
+    ref = o.chunk_stream(data, mn, av, mx).tolist()
+    out, cur, R, i = [], 0, 0, 0
+    while True:
+        if R - cur < mx:
+            if cur + 10 * mx > E:
+                out.append(("err", cur, E))
+                break
+            R = cur + 10 * mx
+        while ref[i] <= cur:
+            i += 1
+        out.append(("chunk", cur, ref[i]))
+        cur = ref[i]
+    if resume:
+        tail = o.chunk_stream(data[E:], mn, av, mx).tolist()
+        s = E
+        for e in tail:
+            out.append(("chunk", s, E + e))
+            s = E + e
+    return out
+
+
+@pytest.mark.parametrize("E,resume", [(100_000, False), ((5 << 20) + 123, False),
+                                      ((5 << 20) + 123, True), ((70 << 20) + 7, True)])
+def test_stream_reader_error(dctx, E, resume):
+    """chunker.go:207-211: a reader error returns the buffered bytes with the
+    error, where the reference's fillBuffer would hit it; then chunking
+    restarts behind them (resume) or the stream ends."""
+    import desync_amd
+    data = o.synth_uniform(14, 0, (90 << 20) + 11)
+    want = _go_next_with_error(data, E, resume, MIN, AVG, MAX)
+    c = desync_amd.NewChunker(_FailingReader(data.tobytes(), E, resume), MIN, AVG, MAX)
+    got = []
+    while True:
+        try:
+            s, b = c.Next()
+        except desync_amd.ChunkerReadError as e:
+            assert bytes(e.chunk) == data[e.start:e.start + len(e.chunk)].tobytes()
+            assert isinstance(e.__cause__, OSError)
+            got.append(("err", e.start, e.start + len(e.chunk)))
+            continue
+        if not b:
+            break
+        assert bytes(b) == data[s:s + len(b)].tobytes()
+        got.append(("chunk", s, s + len(b)))
+    assert got == want
+
+
 def test_two_chunkers_interleaved(dctx):
     """Each Chunker is independent: Next() alternated between two
     streams over different data returns each stream's own chunks; a second
