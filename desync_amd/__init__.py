@@ -8,6 +8,7 @@ mirror of the reference's Go API for that path:
     NewChunker / Chunker.Next / Advance / Min / Avg / Max   (chunker.go)
     IndexFromFile, ChunkingStats                            (make.go)
     VerifyIndex                                             (verifyindex.go)
+    ChunkStream, ChunkStorage                               (index.go, chunkstorage.go)
     Index, IndexChunk, Index.WriteTo, IndexFromReader       (index.go)
     Digest (SHA512256 / SHA256), NullChunk                  (digest.go)
 
@@ -17,13 +18,14 @@ from .chunker import ChunkerReadError, ChunkerWindowSize, Chunker, NewChunker, P
 from .digest import SHA256, SHA512256, NewNullChunk, NullChunk, set_digest  # noqa: F401
 from .errors import Interrupted  # noqa: F401
 from .index import FormatIndex, Index, IndexChunk, IndexFromReader  # noqa: F401
+from .stream import Chunk, ChunkStorage, ChunkStream, MemoryStore  # noqa: F401
 from .make import ChunkingStats, IndexFromFile, VerifyError, VerifyIndex, chunk_ids, cut_device, cut_device_result, \
     cut_fd, cut_host, file_size, index_fd, index_host  # noqa: F401
 
 __all__ = [
     "ChunkerWindowSize", "Chunker", "ChunkerReadError", "NewChunker", "Params", "SHA256", "SHA512256", "NullChunk",
     "NewNullChunk", "set_digest", "Interrupted", "FormatIndex", "Index", "IndexChunk",
-    "IndexFromReader", "ChunkingStats", "IndexFromFile", "cut_device", "cut_device_result",
+    "IndexFromReader", "Chunk", "ChunkStorage", "ChunkStream", "MemoryStore", "ChunkingStats", "IndexFromFile", "cut_device", "cut_device_result",
     "cut_fd", "cut_host", "chunk_ids", "VerifyIndex", "VerifyError", "file_size", "index_fd",
     "index_host",
 ]

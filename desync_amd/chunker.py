@@ -81,6 +81,7 @@ class Chunker:
         self._own = ctx is None
         self.ctx = _lib.Context(device) if ctx is None else ctx
         check(lib().dsx_stream_begin(self.ctx.h, ctypes.byref(self.params.c)), self.ctx.h)
+        self.ctx._stream_owner = self  # (close() must not end a later Chunker's stream)
         self._eof = False
         self._start = ctypes.c_uint64()
         self._size = ctypes.c_uint64()
@@ -124,6 +125,18 @@ class Chunker:
                 continue
             self._fill()
 
+    def EnableIDs(self, algo=None):
+        """Compute every chunk's Digest.Sum on the GPU next to its cut (for
+        ChunkStream); only before the first Next().  ``algo``: "sha512-256"
+        or "sha256" (default: the package-global Digest)."""
+        from . import make
+        check(lib().dsx_stream_ids(self.ctx.h, make._digest_code(algo)), self.ctx.h)
+
+    def ChunkID(self):
+        """The 32-byte ID of the chunk the last Next() returned (EnableIDs)."""
+        p = lib().dsx_stream_chunk_id(self.ctx.h)
+        return ctypes.string_at(p, 32) if p else None
+
     def Advance(self, n):
         """Skip n bytes and restart the hash as if the stream began there."""
         check(lib().dsx_stream_advance(self.ctx.h, int(n)), self.ctx.h)
@@ -142,7 +155,9 @@ class Chunker:
     def close(self):
         """Release the stream (and the context, if this Chunker created it)."""
         if self.ctx is not None and self.ctx.h:
-            lib().dsx_stream_end(self.ctx.h)
+            if getattr(self.ctx, "_stream_owner", None) is self:
+                lib().dsx_stream_end(self.ctx.h)
+                self.ctx._stream_owner = None
             if self._own:
                 self.ctx.close()
         self.ctx = None

@@ -853,7 +853,9 @@ extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_
 // Enqueues digest_kernel on the ctx stream.  max_n bounds the chunk count
 // (the grid is sized from it; with da.range_lo the count is read on the
 // device).
-int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo) {
+int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream,
+                  uint32_t* queue) {
+  if (!stream) stream = c->stream;
   // Lanes: exactly the workgroups that are resident at once (occupancy is set
   // by VGPRs: 2 per CU for SHA-512, 3 for SHA-256), every lane pulling chunks
   // from the queue.  A larger grid would hand its non-resident workgroups a
@@ -869,16 +871,19 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo) {
   const uint64_t blocks = std::max<uint64_t>(
       1, std::min<uint64_t>((max_n + kDigestThreads - 1) / kDigestThreads,
                             (uint64_t)per_cu * (uint64_t)c->ncu));
-  HIPCHK(c, c->dg_queue.ensure(1));
-  HIPCHK(c, hipMemsetAsync(c->dg_queue.p, 0, 4, c->stream));
-  da.queue = c->dg_queue.p;
+  if (!queue) {
+    HIPCHK(c, c->dg_queue.ensure(1));
+    queue = c->dg_queue.p;
+  }
+  HIPCHK(c, hipMemsetAsync(queue, 0, 4, stream));
+  da.queue = queue;
   da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * kDigestThreads);
   if (algo == DSX_DIGEST_SHA512_256)
     hipLaunchKernelGGL(digest_kernel<Sha512>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
-                       c->stream, da);
+                       stream, da);
   else
     hipLaunchKernelGGL(digest_kernel<Sha256>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
-                       c->stream, da);
+                       stream, da);
   HIPCHK(c, hipGetLastError());
   return DSX_OK;
 }

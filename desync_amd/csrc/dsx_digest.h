@@ -31,6 +31,9 @@ struct DigestArgs {
 // snapshot after a window's stitch)
 struct DevState;
 __global__ void state_snapshot_kernel(const DevState* st, uint64_t* rec);
+// a streaming batch starts: rec = {0, entry cut} (fresh: `carry`, else the
+// carried chain position), and a carried chain's cut count restarts at 0
+__global__ void batch_begin_kernel(DevState* st, uint64_t* rec, int fresh, uint64_t carry);
 
 #ifndef DSX_DIGEST_THREADS
 #define DSX_DIGEST_THREADS 256

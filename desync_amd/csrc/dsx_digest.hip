@@ -295,6 +295,14 @@ __global__ void state_snapshot_kernel(const DevState* st, uint64_t* rec) {
   }
 }
 
+__global__ void batch_begin_kernel(DevState* st, uint64_t* rec, int fresh, uint64_t carry) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    rec[0] = 0;
+    rec[1] = fresh ? carry : st->carry;
+    if (!fresh) st->total = 0;
+  }
+}
+
 template <class H>
 __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
   constexpr int BLK = H::BLK;

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <atomic>
 #include <deque>
 #include <string>
@@ -123,7 +124,7 @@ struct dsx_ctx {
     static constexpr int kSlots = 3;  // batches on the GPU at once
     struct Batch {
       uint64_t P, len, seq;
-      bool last;
+      bool last, ids;
       int slot;
     };
     bool active = false, eof = false, done = false, final_pending = false;
@@ -143,13 +144,24 @@ struct dsx_ctx {
     std::deque<Batch> fly;      // batches on the GPU, oldest first
     int next_slot = 0;
     const uint8_t* last_chunk = nullptr;
+    // chunk IDs computed next to the cuts (ChunkStream, dsx_stream_ids)
+    int ids = -1;                                  // DSX_DIGEST_* or -1
+    std::deque<std::array<uint8_t, 32>> idq;       // IDs of the queued cuts
+    uint8_t last_id[32] = {};
+    bool has_id = false;
+    hipStream_t dg_stream = nullptr;               // digests overlap the next batch's scan
     // per-slot resources
     DevBuf<uint8_t> dbuf[kSlots];
     DevBuf<uint64_t> dout[kSlots];
     uint64_t* hcut[kSlots] = {};
     uint64_t hcut_cap[kSlots] = {};
     HostState* hstate = nullptr;  // pinned, kSlots entries
-    hipEvent_t copy_ev[kSlots] = {}, done_ev[kSlots] = {};
+    hipEvent_t copy_ev[kSlots] = {}, done_ev[kSlots] = {}, stitch_ev[kSlots] = {};
+    DevBuf<uint8_t> dids[kSlots];
+    uint8_t* hids[kSlots] = {};
+    uint64_t hids_cap[kSlots] = {};
+    DevBuf<uint64_t> rng;     // per slot {0, entry cut} {cuts, exit cut}: the digest range
+    DevBuf<uint32_t> dq;      // per slot digest queue counters
   } st;
 
   // multi-GPU shard state (dsx_shard_local -> dsx_shard_resolve)
@@ -238,6 +250,9 @@ int read_state(dsx_ctx* c, HostState* out);
 int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_t halo,
                   uint64_t P, uint64_t len, bool is_last);
 int ensure_attr_walk(dsx_ctx* c);
-int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo);
+// digest_kernel on `stream` (null: the ctx stream) with queue counter `queue`
+// (null: the ctx's); max_n bounds the chunk count (sizes the grid)
+int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream = nullptr,
+                  uint32_t* queue = nullptr);
 void index_release(dsx_ctx* c);   // dsx_index.cpp: frees the pipeline's buffers
 void stream_release(dsx_ctx* c);  // dsx_stream.cpp: frees the stream's buffers

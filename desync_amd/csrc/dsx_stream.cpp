@@ -33,8 +33,18 @@ int st_setup(dsx_ctx* c) {
   for (int i = 0; i < kSlots; ++i) {
     if (!s.copy_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&s.copy_ev[i], hipEventDisableTiming));
     if (!s.done_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&s.done_ev[i], hipEventDisableTiming));
+    if (!s.stitch_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&s.stitch_ev[i], hipEventDisableTiming));
   }
+  if (!s.dg_stream) HIPCHK(c, hipStreamCreateWithFlags(&s.dg_stream, hipStreamNonBlocking));
+  HIPCHK(c, grow(c, s.rng, 4 * kSlots));
+  HIPCHK(c, grow(c, s.dq, kSlots));
   return DSX_OK;
+}
+
+// Bytes re-sent in front of a batch: the scan's 48-byte warm-up, and with
+// chunk IDs the whole unfinished chunk (the carried cut is > P - max).
+uint64_t st_halo(const Stream& s) {
+  return s.ids >= 0 ? (s.p.max + 64 + kLine - 1) / kLine * kLine : kHalo;
 }
 
 // Waits for every batch on the GPU and forgets their results.
@@ -42,6 +52,7 @@ int st_drain(dsx_ctx* c) {
   auto& s = c->st;
   HIPCHK(c, hipStreamSynchronize(c->copy_stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (s.dg_stream) HIPCHK(c, hipStreamSynchronize(s.dg_stream));
   s.fly.clear();
   return DSX_OK;
 }
@@ -52,8 +63,9 @@ int st_drain(dsx_ctx* c) {
 int st_room(dsx_ctx* c, uint64_t want) {
   auto& s = c->st;
   if (s.h && s.hend - s.hbase + want <= s.hcap) return DSX_OK;
-  uint64_t keep = std::min(s.cur, s.sched >= kHalo ? s.sched - kHalo : 0);
-  if (!s.fly.empty()) keep = std::min(keep, s.fly.front().P >= kHalo ? s.fly.front().P - kHalo : 0);
+  const uint64_t H = st_halo(s);
+  uint64_t keep = std::min(s.cur, s.sched >= H ? s.sched - H : 0);
+  if (!s.fly.empty()) keep = std::min(keep, s.fly.front().P >= H ? s.fly.front().P - H : 0);
   keep = std::max(keep, s.hbase);
   const uint64_t held = s.hend - keep;
   // queued H2D copies read the buffer: they must have landed before it moves
@@ -83,7 +95,8 @@ int st_issue(dsx_ctx* c, uint64_t len, bool last) {
   const int slot = s.next_slot;
   s.next_slot = (slot + 1) % kSlots;
   const uint64_t P = s.sched;
-  const uint64_t halo = std::min<uint64_t>(kHalo, P - std::max(s.hbase, s.origin));
+  const uint64_t halo = std::min<uint64_t>(st_halo(s), P - std::max(s.hbase, s.origin));
+  const bool ids = s.ids >= 0;
   const uint64_t bound = len / s.p.min + 4;
   HIPCHK(c, grow(c, s.dbuf[slot], halo + len + 64));
   HIPCHK(c, grow(c, s.dout[slot], bound));
@@ -95,17 +108,32 @@ int st_issue(dsx_ctx* c, uint64_t len, bool last) {
     HIPCHK(c, hipHostMalloc((void**)&s.hcut[slot], cap * sizeof(uint64_t)));
     s.hcut_cap[slot] = cap;
   }
+  if (ids) {
+    HIPCHK(c, grow(c, s.dids[slot], 32 * bound));
+    if (s.hids_cap[slot] < bound) {
+      if (s.hids[slot]) (void)hipHostFree(s.hids[slot]);
+      s.hids[slot] = nullptr;
+      s.hids_cap[slot] = 0;
+      const uint64_t cap = bound + bound / 4 + 64;
+      HIPCHK(c, hipHostMalloc((void**)&s.hids[slot], 32 * cap));
+      s.hids_cap[slot] = cap;
+    }
+  }
   HIPCHK(c, hipMemcpyAsync(s.dbuf[slot].p, s.h + (P - halo - s.hbase), halo + len,
                            hipMemcpyHostToDevice, c->copy_stream));
   HIPCHK(c, hipEventRecord(s.copy_ev[slot], c->copy_stream));
   HIPCHK(c, hipStreamWaitEvent(c->stream, s.copy_ev[slot], 0));
+  // the batch's entry cut (the digest range starts there) and, for a carried
+  // chain, its cut count restarting at 0 (the batch's cuts start at out[0])
+  uint64_t* rng = s.rng.p + 4 * slot;
+  hipLaunchKernelGGL(batch_begin_kernel, dim3(1), dim3(64), 0, c->stream, (DevState*)c->state.p,
+                     rng, s.fresh ? 1 : 0, s.fresh_carry);
+  HIPCHK(c, hipGetLastError());
   if (s.fresh) {
     int rc = reset_state(c, s.fresh_carry);  // the scan initialises the chain state
     if (rc) return rc;
     s.fresh = false;
   } else {
-    // the chain carries on; the batch's cuts start at out[0]
-    HIPCHK(c, hipMemsetAsync(&c->state.p->total, 0, sizeof(uint64_t), c->stream));
     c->npiece_call = 0;
   }
   CallCfg cc{&s.p, P + len, s.origin, s.origin + kRound, s.dout[slot].p, bound, s.dense};
@@ -121,10 +149,34 @@ int st_issue(dsx_ctx* c, uint64_t len, bool last) {
   }
   c->h_cur = c->h_state;
   if (rc) return rc;
+  hipStream_t out_stream = c->stream;
+  if (ids) {
+    // Digest.Sum of the batch's chunks on a side stream, overlapping the next
+    // batch's scan: [rng[0], rng[2]) from rng[1], all inside dbuf (the halo
+    // holds the unfinished chunk)
+    hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
+                       (const DevState*)c->state.p, rng + 2);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(s.stitch_ev[slot], c->stream));
+    HIPCHK(c, hipStreamWaitEvent(s.dg_stream, s.stitch_ev[slot], 0));
+    DigestArgs da{};
+    da.blob = s.dbuf[slot].p;
+    da.base_off = P - halo;
+    da.len = halo + len;
+    da.ends = s.dout[slot].p;
+    da.ids = s.dids[slot].p;
+    da.range_lo = rng;
+    da.range_hi = rng + 2;
+    rc = launch_digest(c, da, bound, s.ids, s.dg_stream, s.dq.p + slot);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(s.hids[slot], s.dids[slot].p, 32 * bound, hipMemcpyDeviceToHost,
+                             s.dg_stream));
+    out_stream = s.dg_stream;
+  }
   HIPCHK(c, hipMemcpyAsync(s.hcut[slot], s.dout[slot].p, bound * sizeof(uint64_t),
-                           hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipEventRecord(s.done_ev[slot], c->stream));
-  s.fly.push_back({P, len, c->piece_seq, last, slot});
+                           hipMemcpyDeviceToHost, out_stream));
+  HIPCHK(c, hipEventRecord(s.done_ev[slot], out_stream));
+  s.fly.push_back({P, len, c->piece_seq, last, ids, slot});
   s.sched = P + len;
   return DSX_OK;
 }
@@ -158,6 +210,13 @@ int st_collect(dsx_ctx* c) {
     return DSX_E_INTERNAL;
   }
   for (uint64_t i = 0; i < hs.total; ++i) s.cuts.push_back(s.hcut[b.slot][i]);
+  if (b.ids) {
+    for (uint64_t i = 0; i < hs.total; ++i) {
+      std::array<uint8_t, 32> id;
+      memcpy(id.data(), s.hids[b.slot] + 32 * i, 32);
+      s.idq.push_back(id);
+    }
+  }
   s.carry = hs.carry;
   if (b.last) s.done = true;
   s.fly.pop_front();
@@ -172,7 +231,7 @@ int st_pump(dsx_ctx* c, bool sync) {
   while (true) {
     const uint64_t avail = s.hend - s.sched;
     int rc = DSX_OK;
-    if (avail > s.batch || (avail == s.batch && !s.eof)) {
+    if (avail > s.batch) {  // (one byte is held back: the final batch is never empty)
       rc = st_issue(c, s.batch, false);
     } else if (s.eof) {
       if (avail > 0) {
@@ -206,6 +265,8 @@ void st_finish(dsx_ctx* c) {
 void st_restart(dsx_ctx* c, uint64_t at) {
   auto& s = c->st;
   s.cuts.clear();
+  s.idq.clear();
+  s.has_id = false;
   s.origin = s.sched = s.carry = s.fresh_carry = at;
   s.fresh = true;
   s.done = s.final_pending = false;
@@ -224,8 +285,17 @@ void stream_release(dsx_ctx* c) {
     s.hcut[i] = nullptr;
     if (s.copy_ev[i]) (void)hipEventDestroy(s.copy_ev[i]);
     if (s.done_ev[i]) (void)hipEventDestroy(s.done_ev[i]);
-    s.copy_ev[i] = s.done_ev[i] = nullptr;
+    if (s.stitch_ev[i]) (void)hipEventDestroy(s.stitch_ev[i]);
+    s.copy_ev[i] = s.done_ev[i] = s.stitch_ev[i] = nullptr;
+    s.dids[i].release();
+    if (s.hids[i]) (void)hipHostFree(s.hids[i]);
+    s.hids[i] = nullptr;
+    s.hids_cap[i] = 0;
   }
+  s.rng.release();
+  s.dq.release();
+  if (s.dg_stream) (void)hipStreamDestroy(s.dg_stream);
+  s.dg_stream = nullptr;
   if (s.hstate) (void)hipHostFree(s.hstate);
   s.hstate = nullptr;
 }
@@ -248,7 +318,9 @@ extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
   s.active = true;
   s.eof = false;
   s.dense = false;
+  s.ids = -1;
   s.p = *p;
+  s.batch = 32ull << 20;
   if (const char* v = getenv("DSX_STREAM_BATCH"))
     s.batch = std::max<uint64_t>(4096, (uint64_t)atoll(v));
   s.hbase = s.hend = s.cur = s.skip = 0;
@@ -352,6 +424,12 @@ extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
   }
   const uint64_t e = s.cuts.front();
   s.cuts.pop_front();
+  s.has_id = false;
+  if (!s.idq.empty() && s.idq.size() > s.cuts.size()) {  // (cuts and IDs stay aligned from the back)
+    memcpy(s.last_id, s.idq.front().data(), 32);
+    s.idq.pop_front();
+    s.has_id = true;
+  }
   *start = s.cur;
   *size = e - s.cur;
   s.last_chunk = s.h + (s.cur - s.hbase);
@@ -360,6 +438,26 @@ extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
 }
 
 extern "C" const uint8_t* dsx_stream_chunk_data(dsx_ctx_t* c) { return c ? c->st.last_chunk : nullptr; }
+
+extern "C" int dsx_stream_ids(dsx_ctx_t* c, int algo) {
+  if (!c || (algo != -1 && algo != DSX_DIGEST_SHA512_256 && algo != DSX_DIGEST_SHA256))
+    return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active) return DSX_E_STATE;
+  // only before the first batch of a chain: every chunk then has an ID
+  if (!s.fly.empty() || s.sched != s.origin || !s.cuts.empty()) {
+    c->err = "dsx_stream_ids: chunks were already scanned without IDs";
+    return DSX_E_STATE;
+  }
+  s.ids = algo;
+  if (algo >= 0 && !getenv("DSX_STREAM_BATCH"))
+    s.batch = std::max<uint64_t>(s.batch, 128ull << 20);  // digests are latency-bound: bigger batches
+  return DSX_OK;
+}
+
+extern "C" const uint8_t* dsx_stream_chunk_id(dsx_ctx_t* c) {
+  return c && c->st.has_id ? c->st.last_id : nullptr;
+}
 
 extern "C" int dsx_stream_done(dsx_ctx_t* c) {
   if (!c) return 0;

@@ -1,0 +1,111 @@
+"""ChunkStream (index.go:138-234) over the GPU stream: a single-stream
+Chunker feeds chunks to a store and the Index is built in chunk order.
+
+Reference shape: the producer calls Next(), clones the bytes (the slice
+aliases the chunker's buffer, index.go:196-200) and hands them to n workers
+that compute the chunk ID (NewChunk -> Digest.Sum, index.go:165-169) and store
+the chunk through a ChunkStorage (chunkstorage.go: stores each ID once, skips
+IDs the store already has).  Here the chunk IDs come from the GPU, computed
+next to the cuts (dsx_stream_ids), and the n workers only store.  The index
+flags are the reference's: ExcludeNoDump | SHA512256 (index.go:224-230).
+Compression and the concrete stores stay out of scope (a store is any object
+with HasChunk(id) and StoreChunk(chunk)).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import threading
+
+from .index import CaFormatExcludeNoDump, CaFormatSHA512256, FormatIndex, Index, IndexChunk
+
+
+class Chunk:
+    """chunk.go's Chunk, reduced to what a store needs: the ID and the
+    uncompressed bytes."""
+
+    def __init__(self, chunk_id: bytes, data: bytes):
+        self._id = chunk_id
+        self._data = data
+
+    def ID(self) -> bytes:
+        return self._id
+
+    def Data(self) -> bytes:
+        return self._data
+
+
+class ChunkStorage:
+    """chunkstorage.go: stores a chunk once per ID (an in-memory mark, undone
+    if the store fails) and skips IDs the store already has.  Thread-safe."""
+
+    def __init__(self, ws):
+        self.ws = ws
+        self._lock = threading.Lock()
+        self._processed = set()
+
+    def StoreChunk(self, chunk: Chunk):
+        cid = chunk.ID()
+        with self._lock:
+            if cid in self._processed:
+                return
+            self._processed.add(cid)
+        try:
+            if self.ws.HasChunk(cid):
+                return
+            self.ws.StoreChunk(chunk)
+        except BaseException:
+            with self._lock:
+                self._processed.discard(cid)
+            raise
+
+
+class MemoryStore:
+    """A WriteStore in memory (test double; desync's stores are out of scope)."""
+
+    def __init__(self):
+        self.chunks = {}
+        self._lock = threading.Lock()
+
+    def HasChunk(self, cid: bytes) -> bool:
+        with self._lock:
+            return cid in self.chunks
+
+    def StoreChunk(self, chunk: Chunk):
+        with self._lock:
+            self.chunks[chunk.ID()] = chunk.Data()
+
+
+def ChunkStream(ctx, c, ws, n):
+    """index.go:138-234.  ``c`` is a desync_amd Chunker that has not produced
+    a chunk yet (its IDs are switched on here), ``ws`` a store, ``n`` the
+    number of store workers.  ``ctx``: an object with ``done()`` or None; when
+    it reports done the producer stops and the chunks so far form the index,
+    as the reference's select on ctx.Done() does (index.go:203-206).  A
+    reader error (ChunkerReadError) or a store error is raised."""
+    c.EnableIDs()
+    storage = ChunkStorage(ws)
+    chunks = []
+    pending = set()
+    with cf.ThreadPoolExecutor(max_workers=max(1, int(n))) as pool:
+        try:
+            while True:
+                if ctx is not None and getattr(ctx, "done", lambda: False)():
+                    break
+                start, b = c.Next()
+                if not b:
+                    break
+                cid = c.ChunkID()
+                if cid is None:
+                    raise RuntimeError("chunker produced a chunk without a GPU chunk ID")
+                data = bytes(b)  # slices.Clone (index.go:196-200)
+                chunks.append(IndexChunk(ID=cid, Start=start, Size=len(data)))
+                pending.add(pool.submit(storage.StoreChunk, Chunk(cid, data)))
+                if len(pending) >= 4 * max(1, int(n)):  # bounded in-flight work, like the channel
+                    done, pending = cf.wait(pending, return_when=cf.FIRST_COMPLETED)
+                    for f in done:
+                        f.result()
+        finally:
+            for f in cf.as_completed(pending):
+                f.result()
+    return Index(FormatIndex(CaFormatExcludeNoDump | CaFormatSHA512256, c.Min(), c.Avg(), c.Max()),
+                 chunks)

@@ -162,6 +162,15 @@ int dsx_stream_flush(dsx_ctx_t *ctx, uint64_t *start, uint64_t *size);
 int dsx_stream_advance(dsx_ctx_t *ctx, uint64_t n);
 int dsx_stream_done(dsx_ctx_t *ctx);
 const uint8_t *dsx_stream_chunk_data(dsx_ctx_t *ctx);
+/* Chunk IDs next to the cuts (ChunkStream, index.go:138-234: Next() then
+ * Digest.Sum of every chunk, index.go:165-169): with algo = DSX_DIGEST_* each
+ * batch's chunks are hashed on the GPU right after its stitch, on a side
+ * stream that overlaps the next batch.  Only before the first bytes of a
+ * chain are scanned (else DSX_E_STATE).  dsx_stream_chunk_id returns the
+ * 32-byte ID of the chunk the last pop returned (valid until the next call),
+ * or NULL if it has none. */
+int dsx_stream_ids(dsx_ctx_t *ctx, int algo);
+const uint8_t *dsx_stream_chunk_id(dsx_ctx_t *ctx);
 
 /* ---- multi-GPU shards (split-and-align across ranks) ------------------------
  * A blob of total length `total` is range-sharded; rank r holds

@@ -160,3 +160,75 @@ def test_chunk_ids_rejects_malformed_ends(dctx):
         rc = _lib.lib().dsx_chunk_ids(dctx.h, ctypes.c_void_p(t.data_ptr()), 4096, start,
                                       e.ctypes.data, 3, out.ctypes.data, 0, 0)
         assert rc == _lib.DSX_E_INVAL, ends
+
+
+# ---------------------------------------------------------------- ChunkStream
+def test_chunk_stream_golden(golden):
+    """index_test.go:55-112 TestIndexChunking: ChunkStream over
+    testdata/chunker.input, written with WriteTo, is chunker.index byte for
+    byte, and the store holds every chunk."""
+    import desync_amd
+    store = desync_amd.MemoryStore()
+    c = desync_amd.NewChunker(io.BytesIO(golden("chunker.input")), MIN, AVG, MAX)
+    idx = desync_amd.ChunkStream(None, c, store, 10)
+    b = io.BytesIO()
+    idx.WriteTo(b)
+    assert b.getvalue() == golden("chunker.index")
+    want = o.decode_caibx(golden("chunker.index"))["ids"]
+    assert len(want) == 20 and all(store.HasChunk(i) for i in want)
+
+
+@pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
+def test_chunk_stream_large(algo):
+    """300 MiB with repeated blocks through ChunkStream (128 MiB GPU batches,
+    IDs on the side stream): every cut and ID against the oracle / hashlib,
+    repeated chunks stored once; the index flags are the reference's fixed
+    ExcludeNoDump|SHA512256 (index.go:226) whatever the digest."""
+    import desync_amd
+    from desync_amd import digest
+    blk = o.synth_uniform(43, 0, 8 << 20)
+    parts = [o.synth_uniform(44, 0, 100 << 20), blk, np.zeros(3 << 20, np.uint8), blk,
+             o.synth_uniform(45, 0, 150 << 20), blk, o.synth_uniform(46, 0, (30 << 20) + 17)]
+    data = np.concatenate(parts)
+    store = desync_amd.MemoryStore()
+    prev = digest.Digest.Algorithm()
+    desync_amd.set_digest(algo)
+    try:
+        c = desync_amd.NewChunker(io.BytesIO(data.tobytes()), MIN, AVG, MAX)
+        idx = desync_amd.ChunkStream(None, c, store, 4)
+    finally:
+        desync_amd.set_digest(prev)
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    assert [ch.Start + ch.Size for ch in idx.Chunks] == ref.tolist()
+    want = _ids(data, ref, algo)
+    assert [ch.ID for ch in idx.Chunks] == want
+    assert len(store.chunks) == len(set(want)) < len(want)
+    assert idx.Index.FeatureFlags == o.CA_FORMAT_EXCLUDE_NO_DUMP | o.CA_FORMAT_SHA512256
+
+
+def test_chunk_stream_errors():
+    """A failing store raises out of ChunkStream; a cancelled ctx stops the
+    producer and returns the chunks so far (index.go:203-206)."""
+    import desync_amd
+    data = o.synth_uniform(47, 0, 20 << 20)
+
+    class Bad(desync_amd.MemoryStore):
+        def StoreChunk(self, chunk):
+            raise IOError("disk full")
+
+    with pytest.raises(IOError, match="disk full"):
+        desync_amd.ChunkStream(None, desync_amd.NewChunker(io.BytesIO(data.tobytes()), MIN, AVG, MAX),
+                               Bad(), 2)
+
+    class After:
+        def __init__(self, k):
+            self.k = k
+
+        def done(self):
+            self.k -= 1
+            return self.k < 0
+
+    idx = desync_amd.ChunkStream(After(5), desync_amd.NewChunker(io.BytesIO(data.tobytes()), MIN,
+                                                                 AVG, MAX), desync_amd.MemoryStore(), 2)
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    assert [ch.Start + ch.Size for ch in idx.Chunks] == ref[:5].tolist()

@@ -44,3 +44,37 @@ def test_file_size_block_device(monkeypatch, tmp_path):
     finally:
         os.close(fd)
     assert calls == [0x80081272]
+
+
+def test_chunk_storage_dedup_and_retry():
+    """chunkstorage.go: an ID is stored once; IDs the store has are skipped;
+    a failed store unmarks the ID so it can be retried."""
+    import pytest
+
+    from desync_amd.stream import Chunk, ChunkStorage, MemoryStore
+
+    class Flaky(MemoryStore):
+        def __init__(self):
+            super().__init__()
+            self.calls = 0
+
+        def StoreChunk(self, chunk):
+            self.calls += 1
+            if self.calls == 1:
+                raise IOError("transient")
+            super().StoreChunk(chunk)
+
+    ws = Flaky()
+    s = ChunkStorage(ws)
+    a, b = Chunk(b"a" * 32, b"x"), Chunk(b"b" * 32, b"y")
+    with pytest.raises(IOError):
+        s.StoreChunk(a)
+    s.StoreChunk(a)
+    s.StoreChunk(a)
+    s.StoreChunk(b)
+    assert ws.calls == 3 and set(ws.chunks) == {b"a" * 32, b"b" * 32}
+    ws2 = MemoryStore()
+    ws2.chunks[b"b" * 32] = b"y"
+    s2 = ChunkStorage(ws2)
+    s2.StoreChunk(b)
+    assert ws2.chunks == {b"b" * 32: b"y"}
