@@ -48,7 +48,8 @@ EXPORTS = (
     "dsx_last_error", "dsx_cancel", "dsx_cut_device", "dsx_sync", "dsx_result", "dsx_cut_host",
     "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
     "dsx_stream_done", "dsx_stream_end", "dsx_stream_chunk_data", "dsx_stream_buffer",
-    "dsx_stream_commit", "dsx_stream_flush", "dsx_stream_ids", "dsx_stream_chunk_id", "dsx_shard_local", "dsx_shard_resolve",
+    "dsx_stream_commit", "dsx_stream_flush", "dsx_stream_ids", "dsx_stream_chunk_id",
+    "dsx_stream_pop_many", "dsx_stream_window", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host",
 )
@@ -145,6 +146,8 @@ def lib():
             "dsx_stream_flush": (i32, [vp, P(u64), P(u64)]),
             "dsx_stream_ids": (i32, [vp, i32]),
             "dsx_stream_chunk_id": (vp, [vp]),
+            "dsx_stream_pop_many": (i32, [vp, vp, vp, u64, P(u64), P(u64)]),
+            "dsx_stream_window": (i32, [vp, P(vp), P(u64), P(u64)]),
             "dsx_stream_chunk_data": (vp, [vp]),
             "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), vp, u32]),
             "dsx_shard_resolve": (i32, [vp, vp, i32, i32, vp, vp, u64, P(u64), u32]),

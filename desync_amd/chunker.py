@@ -28,8 +28,11 @@ from . import _lib
 from ._lib import check, lib
 
 ChunkerWindowSize = 48
-# bytes per reader call: the library sends 32 MiB batches to the GPU
-_READ = 16 << 20
+# bytes per reader call (the library sends 8 MiB batches to the GPU)
+_READ = 8 << 20
+# confirmed chunks taken from the library per call (Next() then serves them
+# without a library call per chunk)
+_POP = 4096
 
 
 class Params:
@@ -95,6 +98,13 @@ class Chunker:
         self._err = None    # pending reader exception ...
         self._E = 0         # ... raised at stream position _E
         self._synced = False
+        # chunks popped from the library, served one per Next()
+        self._ends = (ctypes.c_uint64 * _POP)()
+        self._idbuf = None  # (EnableIDs) their IDs
+        self._q, self._qi, self._qids = [], 0, b""
+        self._n = ctypes.c_uint64()
+        self._win, self._wbase = None, 0  # view of the library's held bytes
+        self._last_id = None
 
     # -- reference API -----------------------------------------------------
     def Next(self):
@@ -109,12 +119,18 @@ class Chunker:
             if self._err is not None and target > self._E:
                 return self._read_error()
             self._R = target
+        if self._qi < len(self._q):
+            return self._take()
         while True:
-            rc = check(L.dsx_stream_pop(h, ctypes.byref(self._start), ctypes.byref(self._size)), h)
+            rc = check(L.dsx_stream_pop_many(h, self._ends, self._idbuf, _POP, ctypes.byref(self._start),
+                                             ctypes.byref(self._n)), h)
             if rc == 1:
-                n = self._size.value
-                self._cur = self._start.value + n
-                return self._start.value, _view(L.dsx_stream_chunk_data(h), n)
+                k = self._n.value
+                self._q, self._qi = self._ends[:k], 0
+                if self._idbuf is not None:
+                    self._qids = bytes(self._idbuf)[:32 * k]
+                self._win = None
+                return self._take()
             if self._eof:
                 return self._start.value, memoryview(b"")
             if self._err is not None:
@@ -125,21 +141,37 @@ class Chunker:
                 continue
             self._fill()
 
+    def _take(self):
+        """The next popped chunk as a view of the library's buffer."""
+        if self._win is None:  # (re)map the held bytes after any buffer call
+            base, pos, n = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64()
+            check(lib().dsx_stream_window(self.ctx.h, ctypes.byref(base), ctypes.byref(pos),
+                                          ctypes.byref(n)), self.ctx.h)
+            self._win, self._wbase = _view(base.value or 0, n.value), pos.value
+        i = self._qi
+        s, e = self._cur, self._q[i]
+        self._qi = i + 1
+        self._cur = e
+        if self._idbuf is not None:
+            self._last_id = self._qids[32 * i:32 * i + 32]
+        return s, self._win[s - self._wbase:e - self._wbase]
+
     def EnableIDs(self, algo=None):
         """Compute every chunk's Digest.Sum on the GPU next to its cut (for
         ChunkStream); only before the first Next().  ``algo``: "sha512-256"
         or "sha256" (default: the package-global Digest)."""
         from . import make
         check(lib().dsx_stream_ids(self.ctx.h, make._digest_code(algo)), self.ctx.h)
+        self._idbuf = (ctypes.c_uint8 * (32 * _POP))()
 
     def ChunkID(self):
         """The 32-byte ID of the chunk the last Next() returned (EnableIDs)."""
-        p = lib().dsx_stream_chunk_id(self.ctx.h)
-        return ctypes.string_at(p, 32) if p else None
+        return self._last_id
 
     def Advance(self, n):
         """Skip n bytes and restart the hash as if the stream began there."""
         check(lib().dsx_stream_advance(self.ctx.h, int(n)), self.ctx.h)
+        self._q, self._qi, self._win = [], 0, None
         self._cur += int(n)
         self._R = max(self._R, self._cur)
 
@@ -186,11 +218,13 @@ class Chunker:
         start, n = self._start.value, self._size.value
         chunk = bytes(_view(L.dsx_stream_chunk_data(h), n))
         err, self._err, self._synced = self._err, None, False
+        self._q, self._qi, self._win = [], 0, None
         self._cur = self._R = start + n
         raise ChunkerReadError(start, chunk, err)
 
     def _fill(self):
         L, h = lib(), self.ctx.h
+        self._win = None  # the library may move its buffer
         check(L.dsx_stream_buffer(h, _READ, ctypes.byref(self._ptr)), h)
         try:
             if hasattr(self.r, "readinto"):

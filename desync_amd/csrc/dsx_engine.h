@@ -135,6 +135,7 @@ struct dsx_ctx {
     uint8_t* h = nullptr;          // pinned host buffer: stream bytes [hbase, hend)
     uint64_t hcap = 0, hbase = 0, hend = 0;
     uint64_t cur = 0;     // consumer position (start of the next chunk)
+    uint64_t pin = 0;     // start of the chunks the last pop returned (kept until the next pop)
     uint64_t origin = 0;  // chain origin (0, an Advance target, a read-error restart)
     uint64_t sched = 0;   // bytes before this have been handed to the GPU
     uint64_t carry = 0;   // chain position after the collected batches

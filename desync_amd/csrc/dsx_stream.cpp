@@ -4,7 +4,7 @@
 //
 // The reader's bytes land in a pinned host buffer (dsx_stream_buffer hands
 // out the write pointer, so a reader can fill it directly; dsx_stream_push
-// copies).  Every `batch` bytes (32 MiB) the library enqueues, without
+// copies).  Every `batch` bytes (8 MiB) the library enqueues, without
 // waiting: H2D of the batch on the copy stream, then scan + stitch on the
 // compute stream with the chain state carried on the device, then D2H of the
 // batch's cuts into pinned memory.  Up to three batches are on the GPU while
@@ -64,18 +64,22 @@ int st_room(dsx_ctx* c, uint64_t want) {
   auto& s = c->st;
   if (s.h && s.hend - s.hbase + want <= s.hcap) return DSX_OK;
   const uint64_t H = st_halo(s);
-  uint64_t keep = std::min(s.cur, s.sched >= H ? s.sched - H : 0);
+  uint64_t keep = std::min(std::min(s.cur, s.pin), s.sched >= H ? s.sched - H : 0);
   if (!s.fly.empty()) keep = std::min(keep, s.fly.front().P >= H ? s.fly.front().P - H : 0);
   keep = std::max(keep, s.hbase);
   const uint64_t held = s.hend - keep;
   // queued H2D copies read the buffer: they must have landed before it moves
   for (const auto& b : s.fly) HIPCHK(c, hipEventSynchronize(s.copy_ev[b.slot]));
-  if (held + want <= s.hcap && keep > s.hbase) {
+  // move the held bytes down while that is cheap (at most a quarter of the
+  // buffer); otherwise grow the buffer (up to 32 batches) so that moves stay
+  // rare next to the bytes streamed through
+  const bool cheap = 4 * (held + want) <= s.hcap || s.hcap >= 32 * s.batch;
+  if (held + want <= s.hcap && keep > s.hbase && cheap) {
     memmove(s.h, s.h + (keep - s.hbase), held);
     s.hbase = keep;
     return DSX_OK;
   }
-  uint64_t ncap = std::max<uint64_t>(s.hcap ? s.hcap : 4 * s.batch, 4 * s.batch);
+  uint64_t ncap = std::max<uint64_t>(s.hcap ? 2 * s.hcap : 4 * s.batch, 4 * s.batch);
   while (ncap < held + want) ncap *= 2;
   uint8_t* n = nullptr;
   HIPCHK(c, hipHostMalloc((void**)&n, ncap));
@@ -267,6 +271,7 @@ void st_restart(dsx_ctx* c, uint64_t at) {
   s.cuts.clear();
   s.idq.clear();
   s.has_id = false;
+  s.pin = at;
   s.origin = s.sched = s.carry = s.fresh_carry = at;
   s.fresh = true;
   s.done = s.final_pending = false;
@@ -320,7 +325,7 @@ extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
   s.dense = false;
   s.ids = -1;
   s.p = *p;
-  s.batch = 32ull << 20;
+  s.batch = 8ull << 20;
   if (const char* v = getenv("DSX_STREAM_BATCH"))
     s.batch = std::max<uint64_t>(4096, (uint64_t)atoll(v));
   s.hbase = s.hend = s.cur = s.skip = 0;
@@ -433,11 +438,50 @@ extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
   *start = s.cur;
   *size = e - s.cur;
   s.last_chunk = s.h + (s.cur - s.hbase);
+  s.pin = s.cur;
   s.cur = e;
   return 1;
 }
 
 extern "C" const uint8_t* dsx_stream_chunk_data(dsx_ctx_t* c) { return c ? c->st.last_chunk : nullptr; }
+
+extern "C" int dsx_stream_pop_many(dsx_ctx_t* c, uint64_t* ends, uint8_t* ids, uint64_t cap,
+                                   uint64_t* start, uint64_t* n) {
+  if (!c || !start || !n || (cap && !ends)) return DSX_E_INVAL;
+  *n = 0;
+  uint64_t size = 0;
+  int rc = dsx_stream_pop(c, start, &size);  // collects a batch if needed
+  if (rc <= 0) return rc;
+  auto& s = c->st;
+  const uint64_t first = *start;
+  uint64_t k = 0;
+  while (true) {
+    ends[k] = s.cur;
+    if (ids) {
+      if (!s.has_id) return k ? 1 : DSX_E_STATE;  // (IDs were not switched on)
+      memcpy(ids + 32 * k, s.last_id, 32);
+    }
+    ++k;
+    if (k >= cap || s.cuts.empty()) break;
+    uint64_t st0, sz;
+    rc = dsx_stream_pop(c, &st0, &sz);
+    if (rc <= 0) break;
+  }
+  *n = k;
+  s.last_chunk = s.h + (first - s.hbase);  // the popped chunks, contiguous from here
+  s.pin = first;                            // ... and held until the next pop
+  return 1;
+}
+
+extern "C" int dsx_stream_window(dsx_ctx_t* c, const uint8_t** base, uint64_t* base_pos,
+                                 uint64_t* len) {
+  if (!c || !base || !base_pos || !len) return DSX_E_INVAL;
+  const auto& s = c->st;
+  *base = s.h;
+  *base_pos = s.hbase;
+  *len = s.hend - s.hbase;
+  return DSX_OK;
+}
 
 extern "C" int dsx_stream_ids(dsx_ctx_t* c, int algo) {
   if (!c || (algo != -1 && algo != DSX_DIGEST_SHA512_256 && algo != DSX_DIGEST_SHA256))

@@ -131,8 +131,8 @@ int dsx_cut_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, const dsx_par
  * commit: the caller wrote n bytes at *ptr.  flags: DSX_STREAM_EOF marks the
  *         end of input; DSX_STREAM_SYNC means no more input is coming for
  *         now (a failed reader): everything held is scanned and collected.
- *         Full 32 MiB batches are sent to the GPU without waiting (H2D +
- *         scan + stitch, up to 3 batches in flight).
+ *         Full 8 MiB batches (128 MiB with chunk IDs) are sent to the GPU
+ *         without waiting (H2D + scan + stitch, up to 3 batches in flight).
  * push:   buffer + memcpy + commit (eof != 0: DSX_STREAM_EOF).
  * pop:    start and size of the next confirmed chunk.  Returns 1 if a chunk
  *         was produced, 0 if more input is needed first (or the stream
@@ -170,6 +170,16 @@ const uint8_t *dsx_stream_chunk_data(dsx_ctx_t *ctx);
  * 32-byte ID of the chunk the last pop returned (valid until the next call),
  * or NULL if it has none. */
 int dsx_stream_ids(dsx_ctx_t *ctx, int algo);
+/* Up to cap confirmed chunks at once (a binding that hands out Next() results
+ * without a call per chunk): the first starts at *start, chunk i ends at
+ * ends[i]; with ids non-NULL (dsx_stream_ids on) their 32-byte IDs.  Returns
+ * 1 with *n >= 1, or what dsx_stream_pop returns (0: input needed / ended).
+ * The chunks' bytes are contiguous from dsx_stream_chunk_data(). */
+int dsx_stream_pop_many(dsx_ctx_t *ctx, uint64_t *ends, uint8_t *ids, uint64_t cap,
+                        uint64_t *start, uint64_t *n);
+/* The held stream bytes [*base_pos, *base_pos + *len) at *base (host memory,
+ * valid until the next buffer/commit/push/advance/flush/end on ctx). */
+int dsx_stream_window(dsx_ctx_t *ctx, const uint8_t **base, uint64_t *base_pos, uint64_t *len);
 const uint8_t *dsx_stream_chunk_id(dsx_ctx_t *ctx);
 
 /* ---- multi-GPU shards (split-and-align across ranks) ------------------------
