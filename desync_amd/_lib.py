@@ -36,11 +36,13 @@ DSX_E_IO = -11
 DSX_E_STATE = -12
 DSX_E_INTERNAL = -13
 DSX_E_RESYNC = -14
+DSX_E_PEER = -15
 DSX_STREAM_EOF = 1
 DSX_STREAM_SYNC = 2
 DSX_SEAM_DEVICE = 8
 DSX_SEAM_LAST = 1
 DSX_SEAM_REWALKED = 2
+DSX_SEAM_ERROR = 4
 
 # every symbol include/dsx.h declares (tests check the library exports them)
 EXPORTS = (
@@ -49,9 +51,9 @@ EXPORTS = (
     "dsx_cut_fd", "dsx_stream_begin", "dsx_stream_push", "dsx_stream_pop", "dsx_stream_advance",
     "dsx_stream_done", "dsx_stream_end", "dsx_stream_chunk_data", "dsx_stream_buffer",
     "dsx_stream_commit", "dsx_stream_flush", "dsx_stream_ids", "dsx_stream_chunk_id",
-    "dsx_stream_pop_many", "dsx_stream_window", "dsx_shard_local", "dsx_shard_resolve",
+    "dsx_stream_pop_many", "dsx_stream_window", "dsx_stream_unpop", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
-    "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host",
+    "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host", "dsx_copy",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -148,6 +150,7 @@ def lib():
             "dsx_stream_chunk_id": (vp, [vp]),
             "dsx_stream_pop_many": (i32, [vp, vp, vp, u64, P(u64), P(u64)]),
             "dsx_stream_window": (i32, [vp, P(vp), P(u64), P(u64)]),
+            "dsx_stream_unpop": (i32, [vp, u64]),
             "dsx_stream_chunk_data": (vp, [vp]),
             "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), vp, u32]),
             "dsx_shard_resolve": (i32, [vp, vp, i32, i32, vp, vp, u64, P(u64), u32]),
@@ -156,6 +159,7 @@ def lib():
             "dsx_gen_dedup": (i32, [vp, vp, u64, u64, u64, ctypes.c_double]),
             "dsx_chunk_ids": (i32, [vp, vp, u64, u64, vp, u64, vp, u32, i32]),
             "dsx_get_stats": (i32, [vp, P(Stats)]),
+            "dsx_copy": (i32, [vp, vp, vp, u64]),
             "dsx_index_fd": (i32, [vp, i32, u64, u64, P(Params), i32, vp, vp, u64, P(u64)]),
             "dsx_index_host": (i32, [vp, vp, u64, P(Params), i32, vp, vp, u64, P(u64)]),
             "dsx_debug_trace": (i32, [vp, vp, u64, P(u64), P(u64)]),

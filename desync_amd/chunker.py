@@ -170,7 +170,9 @@ class Chunker:
 
     def Advance(self, n):
         """Skip n bytes and restart the hash as if the stream began there."""
-        check(lib().dsx_stream_advance(self.ctx.h, int(n)), self.ctx.h)
+        h = self.ctx.h
+        check(lib().dsx_stream_unpop(h, self._cur), h)  # (chunks popped ahead go back)
+        check(lib().dsx_stream_advance(h, int(n)), h)
         self._q, self._qi, self._win = [], 0, None
         self._cur += int(n)
         self._R = max(self._R, self._cur)
@@ -214,6 +216,7 @@ class Chunker:
     # -- internals -------------------------------------------------------------
     def _read_error(self):
         L, h = lib(), self.ctx.h
+        check(L.dsx_stream_unpop(h, self._cur), h)
         check(L.dsx_stream_flush(h, ctypes.byref(self._start), ctypes.byref(self._size)), h)
         start, n = self._start.value, self._size.value
         chunk = bytes(_view(L.dsx_stream_chunk_data(h), n))

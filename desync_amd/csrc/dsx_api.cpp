@@ -29,6 +29,10 @@ using namespace dsx;
 static_assert(sizeof(dsx_seam_t) == 7 * 8 + 4 * 4 + 8 * (DSX_SEAM_MAX_CANDS + DSX_SEAM_MAX_CUTS),
               "dsx_seam_t layout");
 
+static void release_kept(dsx_ctx* c);
+
+constexpr uint64_t kSeamPeerFailed = 0x7FFFFFFFFFFFFFFFull;  // seam_resolve_kernel status
+
 int set_hip_err(dsx_ctx* c, hipError_t e, const char* what) {
   char buf[256];
   snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
@@ -96,6 +100,7 @@ extern "C" const char* dsx_strerror(int code) {
     case DSX_E_STATE: return "invalid stream state";
     case DSX_E_INTERNAL: return "internal error";
     case DSX_E_RESYNC: return "seam records changed: all-gather them again and resolve again";
+    case DSX_E_PEER: return "another rank failed (its seam record carries DSX_SEAM_ERROR)";
     default: return "unknown error";
   }
 }
@@ -218,6 +223,8 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
   c->dg_ends.release(); c->dg_ids.release(); c->dg_queue.release();
   c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
+  release_kept(c);
+  c->zero_word.release();
   c->d_seam.release(); c->d_all.release(); c->d_ext.release(); c->d_info.release(); c->d_emit.release();
   if (c->h_res) (void)hipHostFree(c->h_res);
   c->dbuf[0].release(); c->dbuf[1].release();
@@ -257,6 +264,15 @@ extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const uint64_t k = std::min<uint64_t>(cap, words);
   HIPCHK(c, hipMemcpy(out, c->trace.p, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return DSX_OK;
+}
+
+extern "C" int dsx_copy(dsx_ctx_t* c, void* dst, const void* src, uint64_t n) {
+  if (!c || (n && (!dst || !src))) return DSX_E_INVAL;
+  if (!n) return DSX_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(dst, src, n, hipMemcpyDefault));
   return DSX_OK;
 }
 
@@ -364,8 +380,24 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   c->last_nregions = (uint32_t)nregions;
   c->last_region_cap = rcap;
   HIPCHK(c, grow(c, c->lane_slot, nlanes * LS));
-  HIPCHK(c, grow(c, c->region_cnt, nregions));
-  HIPCHK(c, grow(c, c->region_list, nregions * rcap));
+  // region lists: the context's scratch, or (cc.keep: shards) buffers of
+  // their own that outlive the call, so a re-walk can re-run the stitch
+  // without scanning the bytes again
+  uint32_t *rcnt, *rlist;
+  KeptPiece* kp = nullptr;
+  if (cc.keep) {
+    cc.keep->emplace_back();
+    kp = &cc.keep->back();
+    HIPCHK(c, kp->cnt.ensure(nregions));
+    HIPCHK(c, kp->list.ensure(nregions * rcap));
+    rcnt = kp->cnt.p;
+    rlist = kp->list.p;
+  } else {
+    HIPCHK(c, grow(c, c->region_cnt, nregions));
+    HIPCHK(c, grow(c, c->region_list, nregions * rcap));
+    rcnt = c->region_cnt.p;
+    rlist = c->region_list.p;
+  }
   const uint64_t seq = ++c->piece_seq;
 
   ScanArgs sa{};
@@ -382,8 +414,8 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.lane_slots = LS;
   sa.pf_batches = (uint32_t)c->prefetch_batches;
   sa.lane_slot = c->lane_slot.p;
-  sa.region_cnt = c->region_cnt.p;
-  sa.region_list = c->region_list.p;
+  sa.region_cnt = rcnt;
+  sa.region_list = rlist;
   sa.overflow = c->overflow.p + (seq & 1);
   sa.overflow_next = c->overflow.p + ((seq + 1) & 1);
   sa.queue = c->overflow.p + 2 + (seq & 1);
@@ -469,20 +501,38 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));
-  // ---- stitch geometry ----
+  PieceCands pc{};
+  pc.P = c->last_grid_P;  // region r covers (P' + r*RB, P' + (r+1)*RB]
+  pc.RB = region_bytes;
+  pc.nregions = (uint32_t)nregions;
+  pc.region_cap = rcap;
+  pc.region_cnt = rcnt;
+  pc.region_list = rlist;
+  pc.overflow = sa.overflow;
+  if (kp) {
+    kp->pc = pc;
+    kp->P = P;
+    kp->len = len;
+  }
+  int rc = launch_stitch(c, cc, pc, P, len, is_last, seq, line && c->scan_trace);
+  if (rc) return rc;
+  HIPCHK(c, hipEventRecord(c->pev[3 * pi + 2], c->stream));
+  c->stats.pieces++;
+  return DSX_OK;
+}
+
+// walk -> fixup -> gather for one piece whose candidates are in pc.
+int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t P, uint64_t len,
+                  bool is_last, uint64_t seq, bool trace) {
+  const dsx_params_t* p = cc.p;
+  const uint64_t region_bytes = pc.RB;
   StitchArgs ta{};
   ta.chain.min = p->min;
   ta.chain.max = p->max;
   ta.chain.L = cc.L;
   ta.chain.PE = P + len;
   ta.chain.is_last = is_last ? 1u : 0u;
-  ta.pc.P = c->last_grid_P;  // region r covers (P' + r*RB, P' + (r+1)*RB]
-  ta.pc.RB = region_bytes;
-  ta.pc.nregions = (uint32_t)nregions;
-  ta.pc.region_cap = rcap;
-  ta.pc.region_cnt = c->region_cnt.p;
-  ta.pc.region_list = c->region_list.p;
-  ta.pc.overflow = sa.overflow;
+  ta.pc = pc;
   // the carried cut lies in (P - max, P] (its successor needed bytes >= P)
   const uint64_t anchor = (P > cc.origin + p->max) ? P - p->max : cc.origin;
   const uint64_t seg = std::max<uint64_t>(c->seg_max_mult * p->max, c->seg_floor);
@@ -522,7 +572,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   ta.host_state = c->h_cur;
   ta.seq = seq;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
-  if (c->scan_trace && line && walk_grid <= 65536) {
+  if (trace && walk_grid <= 65536) {
     ta.trace = c->trace.p + 3 * c->trace_n;
     c->trace_walk_n = walk_grid;
   }
@@ -533,8 +583,6 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(gather_kernel, dim3((uint32_t)nseg), dim3(256), 0, c->stream, ta);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->pev[3 * pi + 2], c->stream));
-  c->stats.pieces++;
   return DSX_OK;
 }
 
@@ -968,7 +1016,22 @@ extern "C" int dsx_selftest_boundary(dsx_ctx_t* c, const dsx_params_t* p, int mo
 // Chunks the shard from the cut `entry` (shard_start: speculative, make.go's
 // worker at span*i; or the true entry cut on a re-walk), builds the seam
 // record in c->d_seam, leaves the shard's cuts in c->out and waits.
-static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags) {
+static void release_kept(dsx_ctx* c) {
+  for (auto& k : c->sh.kept) {
+    k.cnt.release();
+    k.list.release();
+  }
+  c->sh.kept.clear();
+}
+
+// Chunks the shard from the cut `entry` (shard_start: speculative, make.go's
+// worker at span*i; or the true entry cut on a re-walk), builds the seam
+// record in c->d_seam, leaves the shard's cuts in c->out and waits.
+// The first run scans the bytes and keeps every piece's candidate lists; a
+// re-walk (rewalk = true) only re-runs the stitch over the kept lists from
+// the new entry: O(candidates), no byte is read again.  (Pieces that needed
+// the dense-candidate path keep no lists; their re-walk scans again.)
+static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk) {
   auto& sh = c->sh;
   const dsx_params_t* p = &sh.p;
   const bool is_last = sh.start + sh.len == sh.total;
@@ -976,33 +1039,58 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags) {
   const uint64_t wend0 = sh.start + std::min<uint64_t>(sh.len, 32 * p->max);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, grow(c, c->d_seam, 1));
+  const bool stitch_only = rewalk && !sh.dense && !sh.kept.empty();
   for (int attempt = 0; attempt < 2; ++attempt) {
     if (c->cancel.load()) return DSX_E_INTERRUPTED;
     HIPCHK(c, grow(c, c->out, need));
-    CallCfg cc{p, sh.total, entry, kRound, c->out.p, need, attempt == 1};
+    const bool dense = attempt == 1 || (rewalk && sh.dense);
+    CallCfg cc{p, sh.total, entry, kRound, c->out.p, need, dense};
     cc.halo0 = sh.start > 0 ? sh.halo : 0;
-    int rc = reset_state(c, entry);
-    if (rc) return rc;
+    int rc = DSX_OK;
     HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
-    const uint64_t piece = cc.dense ? kDensePiece : kPieceMax;
-    for (uint64_t off = 0; off < sh.len; off += piece) {
-      const uint64_t n = std::min(piece, sh.len - off);
-      rc = enqueue_piece(c, cc, sh.d + off, off + cc.halo0, sh.start + off, n,
-                         is_last && off + n == sh.len);
+    if (stitch_only) {
+      HIPCHK(c, c->zero_word.ensure(1));
+      HIPCHK(c, hipMemsetAsync(c->zero_word.p, 0, 4, c->stream));
+      hipLaunchKernelGGL(state_init_kernel, dim3(1), dim3(64), 0, c->stream, (DevState*)c->state.p,
+                         entry);
+      HIPCHK(c, hipGetLastError());
+      c->npiece_call = 0;
+      for (size_t i = 0; i < sh.kept.size() && !rc; ++i) {
+        PieceCands pc = sh.kept[i].pc;
+        pc.overflow = c->zero_word.p;  // (the scan succeeded: no overflow)
+        rc = launch_stitch(c, cc, pc, sh.kept[i].P, sh.kept[i].len,
+                           is_last && i + 1 == sh.kept.size(), ++c->piece_seq, false);
+      }
       if (rc) return rc;
-      if (off == 0) {
-        // the window candidates come from the first piece's region lists
-        PieceCands pc{};
-        pc.P = c->last_grid_P;
-        pc.RB = c->last_region_bytes;
-        pc.nregions = c->last_nregions;
-        pc.region_cap = c->last_region_cap;
-        pc.region_cnt = c->region_cnt.p;
-        pc.region_list = c->region_list.p;
-        pc.overflow = nullptr;
-        hipLaunchKernelGGL(seam_cands_kernel, dim3(1), dim3(64), 0, c->stream, pc, sh.start, wend0,
-                           c->d_seam.p);
-        HIPCHK(c, hipGetLastError());
+      hipLaunchKernelGGL(seam_cands_kernel, dim3(1), dim3(64), 0, c->stream, sh.kept[0].pc,
+                         sh.start, wend0, c->d_seam.p);
+      HIPCHK(c, hipGetLastError());
+    } else {
+      release_kept(c);
+      cc.keep = dense ? nullptr : &sh.kept;
+      sh.dense = dense;
+      rc = reset_state(c, entry);
+      if (rc) return rc;
+      const uint64_t piece = cc.dense ? kDensePiece : kPieceMax;
+      for (uint64_t off = 0; off < sh.len; off += piece) {
+        const uint64_t n = std::min(piece, sh.len - off);
+        rc = enqueue_piece(c, cc, sh.d + off, off + cc.halo0, sh.start + off, n,
+                           is_last && off + n == sh.len);
+        if (rc) return rc;
+        if (off == 0) {
+          // the window candidates come from the first piece's region lists
+          PieceCands pc{};
+          pc.P = c->last_grid_P;
+          pc.RB = c->last_region_bytes;
+          pc.nregions = c->last_nregions;
+          pc.region_cap = c->last_region_cap;
+          pc.region_cnt = cc.keep ? sh.kept[0].cnt.p : c->region_cnt.p;
+          pc.region_list = cc.keep ? sh.kept[0].list.p : c->region_list.p;
+          pc.overflow = nullptr;
+          hipLaunchKernelGGL(seam_cands_kernel, dim3(1), dim3(64), 0, c->stream, pc, sh.start,
+                             wend0, c->d_seam.p);
+          HIPCHK(c, hipGetLastError());
+        }
       }
     }
     hipLaunchKernelGGL(seam_finalize_kernel, dim3(1), dim3(1), 0, c->stream, c->d_seam.p,
@@ -1013,7 +1101,7 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags) {
     HostState st;
     rc = read_state(c, &st);
     if (rc) return rc;
-    if (st.err & kErrDense) {
+    if ((st.err & kErrDense) && !stitch_only) {
       c->stats.dense_fallbacks++;
       continue;
     }
@@ -1068,7 +1156,7 @@ extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
     sh.valid = true;
     return seam_out(c, seam, (flags & DSX_SEAM_DEVICE) != 0);
   }
-  rc = shard_run(c, shard_start, 0u);
+  rc = shard_run(c, shard_start, 0u, false);
   if (rc) return rc;
   sh.valid = true;
   return seam_out(c, seam, (flags & DSX_SEAM_DEVICE) != 0);
@@ -1116,14 +1204,31 @@ extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks
     c->err = "shard: resolve did not publish its result";
     return DSX_E_INTERNAL;
   }
+  if (status == kSeamPeerFailed) {
+    *n_out = 0;
+    return DSX_E_PEER;
+  }
   if (status != 0) {
     // seam `status - 1` did not converge inside its window: its owner re-walks
     // its shard from the true entry cut and republishes its record
     *n_out = 0;
     const int failing = (int)(status - 1);
     if (failing == rank) {
-      int rc = shard_run(c, entry, DSX_SEAM_REWALKED);
-      if (rc) return rc;
+      int rc = shard_run(c, entry, DSX_SEAM_REWALKED, true);
+      if (rc) {
+        // publish the failure in this rank's record: the peers' next resolve
+        // returns DSX_E_PEER (no rank waits for a record forever)
+        const size_t off = offsetof(dsx_seam_t, flags);
+        uint32_t fl = 0;
+        const hipMemcpyKind d2h = seam_dev ? hipMemcpyDeviceToHost : hipMemcpyHostToHost;
+        const hipMemcpyKind h2d = seam_dev ? hipMemcpyHostToDevice : hipMemcpyHostToHost;
+        (void)hipStreamSynchronize(c->stream);
+        if (hipMemcpy(&fl, (const uint8_t*)my_seam + off, 4, d2h) == hipSuccess) {
+          fl |= DSX_SEAM_ERROR;
+          (void)hipMemcpy((uint8_t*)my_seam + off, &fl, 4, h2d);
+        }
+        return rc;
+      }
       c->stats.repaired_segments++;
       rc = seam_out(c, my_seam, seam_dev);
       if (rc) return rc;

@@ -25,6 +25,7 @@ __global__ void scanl_kernel(ScanArgs a);
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);
+__global__ void state_init_kernel(DevState* st, uint64_t carry);
 __global__ void gen_uniform_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed);
 __global__ void gen_dedup_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed,
                                  uint32_t p_thresh);
@@ -75,6 +76,14 @@ struct DevBuf {
 
 }  // namespace dsx_host
 using namespace dsx_host;
+
+// A piece's candidate lists kept past its call (shards: the O(candidates)
+// re-walk re-runs only the stitch over them)
+struct KeptPiece {
+  DevBuf<uint32_t> cnt, list;
+  PieceCands pc{};
+  uint64_t P = 0, len = 0;
+};
 
 struct dsx_ctx {
   int device = 0;
@@ -136,6 +145,8 @@ struct dsx_ctx {
     uint64_t hcap = 0, hbase = 0, hend = 0;
     uint64_t cur = 0;     // consumer position (start of the next chunk)
     uint64_t pin = 0;     // start of the chunks the last pop returned (kept until the next pop)
+    std::vector<uint64_t> grp;                    // ends the last pop_many returned ...
+    std::vector<std::array<uint8_t, 32>> grp_ids; // ... and their IDs (dsx_stream_unpop)
     uint64_t origin = 0;  // chain origin (0, an Advance target, a read-error restart)
     uint64_t sched = 0;   // bytes before this have been handed to the GPU
     uint64_t carry = 0;   // chain position after the collected batches
@@ -172,8 +183,11 @@ struct dsx_ctx {
     dsx_params_t p{};
     uint64_t nspec = 0;  // speculative cuts in ctx->out
     bool valid = false;
+    bool dense = false;                // scanned on the dense path (lists not kept)
+    std::vector<KeptPiece> kept;       // the shard's pieces' region lists
   } sh;
   DevBuf<dsx_seam_t> d_seam, d_all;
+  DevBuf<uint32_t> zero_word;  // an overflow flag that stays 0 (stitch-only re-runs)
   DevBuf<uint64_t> d_ext, d_info, d_emit;
   uint64_t* h_res = nullptr;  // pinned: shard_emit_kernel status / count / entry
 
@@ -243,6 +257,7 @@ struct CallCfg {
   uint64_t out_cap;
   bool dense;        // dense-candidate path
   uint64_t halo0 = 0;  // readable bytes before the first piece (shards)
+  std::vector<KeptPiece>* keep = nullptr;  // keep every piece's region lists here
 };
 
 // engine entry points (dsx_api.cpp)
@@ -251,6 +266,8 @@ int read_state(dsx_ctx* c, HostState* out);
 int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_t halo,
                   uint64_t P, uint64_t len, bool is_last);
 int ensure_attr_walk(dsx_ctx* c);
+int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t P, uint64_t len,
+                  bool is_last, uint64_t seq, bool trace);
 // digest_kernel on `stream` (null: the ctx stream) with queue counter `queue`
 // (null: the ctx's); max_n bounds the chunk count (sizes the grid)
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream = nullptr,

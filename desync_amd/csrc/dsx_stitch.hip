@@ -627,6 +627,20 @@ __global__ __launch_bounds__(kFixThreads) void fixup_kernel(StitchArgs a) {
   }
 }
 
+// The chain state of a stitch-only pass (a shard re-walked from its true
+// entry over kept candidate lists; normally the scan initialises it).
+__global__ void state_init_kernel(DevState* st, uint64_t carry) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    st->carry = carry;
+    st->total = 0;
+    st->piece_cuts = 0;
+    st->repaired = 0;
+    st->done = 0;
+    st->err = 0;
+    st->active = 0;
+  }
+}
+
 // ---- K4: gather the per-segment lists into the contiguous output ---------
 __global__ __launch_bounds__(256) void gather_kernel(StitchArgs a) {
   const uint32_t k = blockIdx.x;
@@ -743,6 +757,14 @@ struct SeamSrc {
 __global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
                                     uint64_t max, uint64_t* ext, uint64_t* info) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int r = 0; r < nranks; ++r) {
+    if (all[r].flags & DSX_SEAM_ERROR) {  // a peer failed: every rank stops
+      info[0] = 0x7FFFFFFFFFFFFFFFull;
+      info[1] = (uint64_t)r;
+      info[2] = 0;
+      return;
+    }
+  }
   uint64_t mine_c = all[rank].shard_start, mine_n = 0;
   uint64_t entry = all[0].exit_cut;
   for (int r = 1; r < nranks; ++r) {

@@ -272,6 +272,8 @@ void st_restart(dsx_ctx* c, uint64_t at) {
   s.idq.clear();
   s.has_id = false;
   s.pin = at;
+  s.grp.clear();
+  s.grp_ids.clear();
   s.origin = s.sched = s.carry = s.fresh_carry = at;
   s.fresh = true;
   s.done = s.final_pending = false;
@@ -455,8 +457,16 @@ extern "C" int dsx_stream_pop_many(dsx_ctx_t* c, uint64_t* ends, uint8_t* ids, u
   auto& s = c->st;
   const uint64_t first = *start;
   uint64_t k = 0;
+  s.grp.clear();
+  s.grp_ids.clear();
   while (true) {
     ends[k] = s.cur;
+    s.grp.push_back(s.cur);
+    if (s.has_id) {
+      std::array<uint8_t, 32> id;
+      memcpy(id.data(), s.last_id, 32);
+      s.grp_ids.push_back(id);
+    }
     if (ids) {
       if (!s.has_id) return k ? 1 : DSX_E_STATE;  // (IDs were not switched on)
       memcpy(ids + 32 * k, s.last_id, 32);
@@ -471,6 +481,25 @@ extern "C" int dsx_stream_pop_many(dsx_ctx_t* c, uint64_t* ends, uint8_t* ids, u
   s.last_chunk = s.h + (first - s.hbase);  // the popped chunks, contiguous from here
   s.pin = first;                            // ... and held until the next pop
   return 1;
+}
+
+extern "C" int dsx_stream_unpop(dsx_ctx_t* c, uint64_t pos) {
+  if (!c) return DSX_E_INVAL;
+  auto& s = c->st;
+  if (!s.active) return DSX_E_STATE;
+  if (pos == s.cur) return DSX_OK;
+  if (pos < s.pin || pos > s.cur) return DSX_E_INVAL;
+  // the chunks of the last group that end after pos go back to the queue
+  const bool with_ids = s.grp_ids.size() == s.grp.size();
+  for (size_t i = s.grp.size(); i-- > 0;) {
+    if (s.grp[i] <= pos) break;
+    s.cuts.push_front(s.grp[i]);
+    if (with_ids) s.idq.push_front(s.grp_ids[i]);
+  }
+  s.cur = pos;
+  s.grp.clear();
+  s.grp_ids.clear();
+  return DSX_OK;
 }
 
 extern "C" int dsx_stream_window(dsx_ctx_t* c, const uint8_t** base, uint64_t* base_pos,

@@ -11,9 +11,20 @@ and speculative cuts of each shard; RCCL over xGMI when the group uses the
 (dsx_shard_resolve) to get its exact slice of the sequential cut list.  A
 seam that does not converge inside its window (a zero run across a shard
 boundary -- README.md:114-119) makes its owner re-walk its shard from the
-true entry cut; the ranks then exchange the records again
-(dsx_shard_resolve returns DSX_E_RESYNC; at most nranks rounds).  The
-collective moves only seam metadata, never blob bytes.
+true entry cut over its kept candidate lists (no byte is scanned again); the
+ranks then exchange the records again (DSX_E_RESYNC; at most nranks rounds).
+A rank whose resolve fails marks its record DSX_SEAM_ERROR and publishes it
+once more, so every peer fails too instead of waiting (DSX_E_PEER).
+
+Chunk IDs across seams (shard_chunk_ids): the chunk that ends at a rank's
+first cut starts in an earlier shard, at most max bytes back; the ranks
+all-gather the tails behind their last cut (the "overlap bytes" of the seams,
+<= max each), and each rank hashes its chunks on its own GPU.
+
+The protocol loop (seam_protocol) is shared by every transport: host records
+over any torch.distributed backend (shard_chunk), HBM records over RCCL
+(DeviceShard, bench.py), and the gloo CPU test, which plugs the oracle's
+restatement of the two library calls into the same loop.
 """
 from __future__ import annotations
 
@@ -22,9 +33,14 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import DSX_E_RESYNC, DSX_OUT_DEVICE, DSX_SEAM_DEVICE, check, lib
+from ._lib import DSX_E_PEER, DSX_E_RESYNC, DSX_OUT_DEVICE, DSX_SEAM_DEVICE, check, lib
 
 SEAM_BYTES = ctypes.sizeof(_lib.Seam)
+FLAGS_OFF = _lib.Seam.flags.offset
+
+
+class PeerFailed(RuntimeError):
+    """Another rank's seam record carries DSX_SEAM_ERROR."""
 
 
 def seam_to_bytes(seam: "_lib.Seam") -> bytes:
@@ -48,6 +64,107 @@ def exchange_seams(seam_bytes: bytes, group=None, device=None) -> bytes:
     return b"".join(b.cpu().numpy().tobytes() for b in bufs)
 
 
+def failed_ranks(all_bytes: bytes, world: int):
+    """Ranks whose record in the gathered bytes carries DSX_SEAM_ERROR."""
+    return [r for r in range(world)
+            if int.from_bytes(all_bytes[r * SEAM_BYTES + FLAGS_OFF:r * SEAM_BYTES + FLAGS_OFF + 4],
+                              "little") & _lib.DSX_SEAM_ERROR]
+
+
+def seam_protocol(engine, world):
+    """The exchange / resolve loop (dsx.h, multi-GPU shards).  ``engine``:
+    local() -> record; exchange(record) -> all records; failed(all) -> ranks
+    with DSX_SEAM_ERROR; resolve(all) -> "ok" | "resync" (raises on a local
+    failure); record() -> the (re-walked) record; mark_error(record) ->
+    record with DSX_SEAM_ERROR; result() -> this rank's cut list."""
+    rec = engine.local()
+    for _ in range(world + 1):
+        allrec = engine.exchange(rec)
+        bad = engine.failed(allrec)
+        if bad:
+            raise PeerFailed(f"rank(s) {bad} failed during seam resolution")
+        try:
+            st = engine.resolve(allrec)
+        except PeerFailed:
+            raise
+        except BaseException:
+            # let the peers see the failure instead of waiting for this rank
+            engine.exchange(engine.mark_error(rec))
+            raise
+        if st == "ok":
+            return engine.result()
+        rec = engine.record()
+    raise RuntimeError("seam resolution did not settle within nranks rounds")
+
+
+def _resolve_rc(rc, h):
+    if rc == DSX_E_RESYNC:
+        return "resync"
+    if rc == DSX_E_PEER:
+        raise PeerFailed("a peer rank failed during seam resolution")
+    check(rc, h)
+    return "ok"
+
+
+class _HostEngine:
+    """Library calls with host-memory seam records, any torch.distributed
+    backend (records through host memory)."""
+
+    def __init__(self, ctx, d_ptr, halo, shard_start, shard_len, total, params, group, device):
+        import torch.distributed as dist
+        self.ctx, self.d_ptr, self.halo = ctx, d_ptr, halo
+        self.start, self.len, self.total, self.params = shard_start, shard_len, total, params
+        self.group, self.device = group, device
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.seam = _lib.Seam()
+        self.cap = shard_len // params.min + 4 + _lib.DSX_SEAM_MAX_CUTS
+        self.out = np.empty(self.cap, dtype=np.uint64)
+        self.n = ctypes.c_uint64()
+
+    def local(self):
+        L, h = lib(), self.ctx.h
+        check(L.dsx_shard_local(h, ctypes.c_void_p(self.d_ptr), self.halo, self.start, self.len,
+                                self.total, ctypes.byref(self.params.c),
+                                ctypes.addressof(self.seam), 0), h)
+        return seam_to_bytes(self.seam)
+
+    def exchange(self, rec):
+        return exchange_seams(rec, self.group, self.device)
+
+    def failed(self, allrec):
+        return failed_ranks(allrec, self.world)
+
+    def resolve(self, allrec):
+        arr = seams_from_bytes(allrec, self.world)
+        rc = lib().dsx_shard_resolve(self.ctx.h, ctypes.addressof(arr), self.world, self.rank,
+                                     ctypes.addressof(self.seam), self.out.ctypes.data, self.cap,
+                                     ctypes.byref(self.n), 0)
+        return _resolve_rc(rc, self.ctx.h)
+
+    def record(self):
+        return seam_to_bytes(self.seam)
+
+    def mark_error(self, rec):
+        b = bytearray(rec)
+        fl = int.from_bytes(b[FLAGS_OFF:FLAGS_OFF + 4], "little") | _lib.DSX_SEAM_ERROR
+        b[FLAGS_OFF:FLAGS_OFF + 4] = fl.to_bytes(4, "little")
+        return bytes(b)
+
+    def result(self):
+        return self.out[:self.n.value].copy()
+
+
+def shard_chunk(d_ptr, halo, shard_start, shard_len, total, params, ctx=None, group=None,
+                device=None):
+    """This rank's exact cut list (np.uint64 chunk end offsets c with
+    shard_start < c <= shard_start + shard_len).  The seam records go through
+    host memory and ``torch.distributed`` (any backend)."""
+    ctx = ctx or _lib.default_context()
+    eng = _HostEngine(ctx, d_ptr, halo, shard_start, shard_len, total, params, group, device)
+    return seam_protocol(eng, eng.world)
+
+
 class DeviceShard:
     """The N>1 path with the seam records in HBM (RCCL all-gather in place).
 
@@ -63,6 +180,7 @@ class DeviceShard:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.nccl = dist.get_backend(group) == "nccl"
         dev = torch.device("cuda", ctx.device)
         self.seam = torch.empty(SEAM_BYTES, dtype=torch.uint8, device=dev)
         self.all = torch.empty(self.world * SEAM_BYTES, dtype=torch.uint8, device=dev)
@@ -70,56 +188,129 @@ class DeviceShard:
         self.out = torch.empty(self.cap, dtype=torch.int64, device=dev)
         self.n = ctypes.c_uint64()
 
-    def run(self):
-        import torch
-        import torch.distributed as dist
+    # -- engine interface (seam_protocol) --------------------------------------
+    def local(self):
         L, h = lib(), self.ctx.h
         check(L.dsx_shard_local(h, ctypes.c_void_p(self.d_ptr), self.halo, self.start, self.len,
                                 self.total, ctypes.byref(self.params.c),
                                 ctypes.c_void_p(self.seam.data_ptr()), DSX_SEAM_DEVICE), h)
-        for _ in range(self.world + 1):
-            if dist.get_backend(self.group) == "nccl":
-                dist.all_gather_into_tensor(self.all, self.seam, group=self.group)
-            else:  # e.g. gloo (CPU tensors only): stage through host memory
-                mine = self.seam.cpu()
-                bufs = [torch.empty_like(mine) for _ in range(self.world)]
-                dist.all_gather(bufs, mine, group=self.group)
-                self.all.copy_(torch.cat(bufs))
-            torch.cuda.current_stream().synchronize()
-            rc = L.dsx_shard_resolve(h, ctypes.c_void_p(self.all.data_ptr()), self.world,
+        return self.seam
+
+    def exchange(self, rec):
+        import torch
+        import torch.distributed as dist
+        if self.nccl:
+            dist.all_gather_into_tensor(self.all, rec, group=self.group)
+        else:  # e.g. gloo (CPU tensors only): stage through host memory
+            mine = rec.cpu()
+            bufs = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(bufs, mine, group=self.group)
+            self.all.copy_(torch.cat(bufs))
+        torch.cuda.current_stream().synchronize()
+        return self.all
+
+    def failed(self, allrec):
+        # the records stay in HBM: dsx_shard_resolve checks their flags on the
+        # device and returns DSX_E_PEER (no host round trip per step)
+        return []
+
+    def resolve(self, allrec):
+        rc = lib().dsx_shard_resolve(self.ctx.h, ctypes.c_void_p(allrec.data_ptr()), self.world,
                                      self.rank, ctypes.c_void_p(self.seam.data_ptr()),
                                      ctypes.c_void_p(self.out.data_ptr()), self.cap,
                                      ctypes.byref(self.n), DSX_SEAM_DEVICE | DSX_OUT_DEVICE)
-            if rc != DSX_E_RESYNC:
-                check(rc, h)
-                return self.n.value
-        raise RuntimeError("seam resolution did not settle within nranks rounds")
+        return _resolve_rc(rc, self.ctx.h)
+
+    def record(self):
+        return self.seam
+
+    def mark_error(self, rec):
+        rec[FLAGS_OFF] = int(rec[FLAGS_OFF].item()) | _lib.DSX_SEAM_ERROR
+        return rec
+
+    def result(self):
+        return self.n.value
+
+    # -- bench step ------------------------------------------------------------
+    def run(self):
+        return seam_protocol(self, self.world)
 
     def cuts(self):
         return self.out[:self.n.value].cpu().numpy().astype(np.uint64)
 
 
-def shard_chunk(d_ptr, halo, shard_start, shard_len, total, params, ctx=None, group=None,
-                device=None):
-    """This rank's exact cut list (np.uint64 chunk end offsets c with
-    shard_start < c <= shard_start + shard_len).  The seam records go through
-    host memory and ``torch.distributed`` (any backend)."""
+# ---------------------------------------------------------------------------
+# chunk IDs across shards
+# ---------------------------------------------------------------------------
+def tail_record(ctx, d_ptr, shard_start, shard_len, cuts, max_size):
+    """This rank's seam tail: {has_cut, length} + the bytes behind its last
+    cut (or, without a cut, its whole shard, < max bytes: a shard of max
+    bytes or more always holds a cut), padded to 16 + max bytes -- the
+    overlap bytes the next rank's first chunk needs."""
+    end = shard_start + shard_len
+    has_cut = len(cuts) > 0
+    t0 = int(cuts[-1]) if has_cut else shard_start
+    n = end - t0
+    if n > max_size:
+        raise ValueError(f"tail of {n} bytes behind the last cut exceeds max")
+    rec = np.zeros(16 + max_size, dtype=np.uint8)
+    rec[:16] = np.frombuffer(np.array([1 if has_cut else 0, n], np.uint64).tobytes(), np.uint8)
+    if n:
+        check(lib().dsx_copy(ctx.h, rec[16:].ctypes.data, ctypes.c_void_p(d_ptr + (t0 - shard_start)),
+                             n), ctx.h)
+    return rec.tobytes()
+
+
+def rank_chunk_ids(ctx, d_ptr, shard_start, shard_len, cuts, tails, rank, algo=None):
+    """IDs of this rank's chunks (those ending at its cuts), given every
+    rank's tail_record (rank order).  The first chunk starts in an earlier
+    shard (at most max bytes back): its prefix is the concatenated tails back
+    to the first rank that has a cut; it is assembled in HBM and hashed with
+    the rest of the shard's chunks by dsx_chunk_ids."""
+    import torch
+
+    from .make import chunk_ids
+    cuts = np.asarray(cuts, dtype=np.uint64)
+    if cuts.size == 0:
+        return []
+    prefix = b""
+    for q in range(rank - 1, -1, -1):
+        head = np.frombuffer(tails[q][:16], np.uint64)
+        n = int(head[1])
+        prefix = tails[q][16:16 + n] + prefix
+        if head[0]:
+            break
+    first = int(cuts[0])
+    head_len = first - shard_start
+    buf = torch.empty(len(prefix) + head_len, dtype=torch.uint8, device=f"cuda:{ctx.device}")
+    if prefix:
+        buf[:len(prefix)].copy_(torch.frombuffer(bytearray(prefix), dtype=torch.uint8))
+        torch.cuda.synchronize()
+    if head_len:
+        check(lib().dsx_copy(ctx.h, ctypes.c_void_p(buf.data_ptr() + len(prefix)),
+                             ctypes.c_void_p(d_ptr), head_len), ctx.h)
+    ids = chunk_ids(buf.data_ptr(), buf.numel(), np.array([buf.numel()], np.uint64), 0, ctx=ctx,
+                    algo=algo)
+    if cuts.size > 1:
+        ids += chunk_ids(d_ptr, shard_len, cuts[1:] - np.uint64(shard_start), head_len, ctx=ctx,
+                         algo=algo)
+    return ids
+
+
+def shard_chunk_ids(d_ptr, shard_start, shard_len, cuts, params, ctx=None, group=None,
+                    device=None, algo=None):
+    """Chunk IDs of this rank's cuts (shard_chunk's result), the seam-straddling
+    chunk included: one all-gather of the <= max-byte tails (the overlap
+    bytes), then dsx_chunk_ids on this rank's GPU."""
+    import torch
     import torch.distributed as dist
     ctx = ctx or _lib.default_context()
-    L, h = lib(), ctx.h
-    seam = _lib.Seam()
-    check(L.dsx_shard_local(h, ctypes.c_void_p(d_ptr), halo, shard_start, shard_len, total,
-                            ctypes.byref(params.c), ctypes.addressof(seam), 0), h)
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    cap = shard_len // params.min + 4 + _lib.DSX_SEAM_MAX_CUTS
-    out = np.empty(cap, dtype=np.uint64)
-    n = ctypes.c_uint64()
-    for _ in range(world + 1):
-        arr = seams_from_bytes(exchange_seams(seam_to_bytes(seam), group, device), world)
-        rc = L.dsx_shard_resolve(h, ctypes.addressof(arr), world, rank, ctypes.addressof(seam),
-                                 out.ctypes.data, cap, ctypes.byref(n), 0)
-        if rc != DSX_E_RESYNC:
-            check(rc, h)
-            return out[:n.value].copy()
-    raise RuntimeError("seam resolution did not settle within nranks rounds")
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    rec = tail_record(ctx, d_ptr, shard_start, shard_len, cuts, params.max)
+    mine = torch.frombuffer(bytearray(rec), dtype=torch.uint8)
+    if device is not None:
+        mine = mine.to(device)
+    bufs = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(bufs, mine, group=group)
+    tails = [b.cpu().numpy().tobytes() for b in bufs]
+    return rank_chunk_ids(ctx, d_ptr, shard_start, shard_len, cuts, tails, rank, algo)

@@ -56,7 +56,8 @@ enum {
     DSX_E_IO = -11,              /* read() on the file descriptor failed */
     DSX_E_STATE = -12,           /* call not valid in the current stream state */
     DSX_E_INTERNAL = -13,        /* internal consistency check failed */
-    DSX_E_RESYNC = -14           /* dsx_shard_resolve: exchange the seam records again */
+    DSX_E_RESYNC = -14,          /* dsx_shard_resolve: exchange the seam records again */
+    DSX_E_PEER = -15             /* dsx_shard_resolve: another rank's record carries DSX_SEAM_ERROR */
 };
 
 /* ---- chunker parameters ----------------------------------------------------
@@ -177,6 +178,11 @@ int dsx_stream_ids(dsx_ctx_t *ctx, int algo);
  * The chunks' bytes are contiguous from dsx_stream_chunk_data(). */
 int dsx_stream_pop_many(dsx_ctx_t *ctx, uint64_t *ends, uint8_t *ids, uint64_t cap,
                         uint64_t *start, uint64_t *n);
+/* Gives back the chunks of the last pop_many that end after pos (a binding
+ * that consumed only some of them before an Advance or a read error): the
+ * consumer position returns to pos (a chunk end of that group) and the
+ * chunks after it are queued again. */
+int dsx_stream_unpop(dsx_ctx_t *ctx, uint64_t pos);
 /* The held stream bytes [*base_pos, *base_pos + *len) at *base (host memory,
  * valid until the next buffer/commit/push/advance/flush/end on ctx). */
 int dsx_stream_window(dsx_ctx_t *ctx, const uint8_t **base, uint64_t *base_pos, uint64_t *len);
@@ -203,7 +209,12 @@ const uint8_t *dsx_stream_chunk_id(dsx_ctx_t *ctx);
  *   that seam has then re-walked its shard from the true entry cut and
  *   rewritten its record `my_seam` (flag DSX_SEAM_REWALKED); every rank
  *   all-gathers the records again and calls dsx_shard_resolve again (at most
- *   nranks rounds).  d_shard passed to dsx_shard_local must stay valid until
+ *   nranks rounds).  The re-walk re-runs only the stitch over the shard's
+ *   kept candidate lists (O(candidates), no byte is scanned again).  If the
+ *   re-walk itself fails, resolve returns that error and marks `my_seam`
+ *   DSX_SEAM_ERROR: the caller all-gathers it once more so that every other
+ *   rank's resolve returns DSX_E_PEER instead of waiting for a record that
+ *   never comes.  d_shard passed to dsx_shard_local must stay valid until
  *   dsx_shard_resolve returns DSX_OK.
  * Seam records are plain bytes. */
 #define DSX_SEAM_MAX_CANDS 1024
@@ -211,6 +222,7 @@ const uint8_t *dsx_stream_chunk_id(dsx_ctx_t *ctx);
 #define DSX_SEAM_DEVICE 8u      /* flag: seam records are device memory */
 #define DSX_SEAM_LAST 1u        /* seam flags: the shard ends the blob */
 #define DSX_SEAM_REWALKED 2u    /* seam flags: chain re-walked from the true entry `entry` */
+#define DSX_SEAM_ERROR 4u       /* seam flags: the owner failed; every rank's resolve returns DSX_E_PEER */
 typedef struct dsx_seam {
     uint64_t shard_start, shard_len, total;
     uint64_t first_cand_beyond;   /* first candidate > window end, or UINT64_MAX */
@@ -228,6 +240,11 @@ int dsx_shard_local(dsx_ctx_t *ctx, const void *d_shard, uint64_t halo, uint64_t
 int dsx_shard_resolve(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, int rank,
                       dsx_seam_t *my_seam, uint64_t *out_ends, uint64_t cap, uint64_t *n_out,
                       uint32_t flags);
+
+/* Synchronous copy of n bytes between any host / device pointers (hipMemcpy
+ * with the direction inferred): a binding without its own GPU runtime uses it
+ * to move the seam-tail bytes of a shard (the chunk IDs across seams). */
+int dsx_copy(dsx_ctx_t *ctx, void *dst, const void *src, uint64_t n);
 
 /* ---- diagnostics ------------------------------------------------------------- */
 /* Evaluates the GPU boundary predicate (mode 0: multiply-inverse form of

@@ -1,0 +1,116 @@
+"""The N>1 path as shipped, on one MI355X: 2 processes share the GPU and talk
+over "gloo" (RCCL needs one GPU per rank; the seam protocol is the same).
+
+* desync_amd.shard.shard_chunk (dsx_shard_local / dsx_shard_resolve through
+  seam_protocol) and shard_chunk_ids (the seam tails all-gathered, IDs on the
+  GPU) in every rank: the concatenated cut lists and IDs equal the oracle's
+  sequential chunking and hashlib (make_test.go:16-80's property), including a
+  zero run across the seam that forces the O(candidates) re-walk.
+* bench.py's DeviceShard path (records in HBM) under torch.distributed.run
+  with --check, as the driver launches it for N > 1.
+"""
+import hashlib
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MIN, AVG, MAX = 16 * 1024, 64 * 1024, 256 * 1024
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _compose(kind):
+    from oracle import oracle as o
+    if kind == "random":
+        return o.synth_uniform(51, 0, (24 << 20) + 999)
+    head = o.synth_uniform(52, 0, 3 * MAX + 12345)
+    return np.concatenate([head, np.zeros(100 * MAX, np.uint8), o.synth_uniform(53, 0, 5 * MAX)])
+
+
+def _worker(rank, world, port, data, q):
+    sys.path.insert(0, REPO)
+    import torch
+    import torch.distributed as dist
+
+    import desync_amd
+    from desync_amd import _lib, shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        total = data.size
+        span = total // world
+        start = rank * span
+        length = span if rank < world - 1 else total - start
+        halo = 64 if rank else 0
+        t = torch.from_numpy(data[start - halo:start + length].copy()).to("cuda:0")
+        torch.cuda.synchronize()
+        p = desync_amd.Params(MIN, AVG, MAX)
+        ctx = _lib.Context(0)
+        cuts = shard.shard_chunk(t.data_ptr() + halo, halo, start, length, total, p, ctx=ctx)
+        pieces = ctx.stats().pieces
+        ids = shard.shard_chunk_ids(t.data_ptr() + halo, start, length, cuts, p, ctx=ctx)
+        out = [None] * world
+        dist.all_gather_object(out, (cuts.tolist(), [i.hex() for i in ids], pieces))
+        if rank == 0:
+            q.put(out)
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["random", "seam-zero-run"])
+def test_shard_chunk_two_processes(kind):
+    import torch.multiprocessing as mp
+
+    from oracle import oracle as o
+    data = _compose(kind)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, data, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cuts = sum((x[0] for x in out), [])
+    ids = sum((x[1] for x in out), [])
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    assert cuts == ref.tolist()
+    raw, s, want = data.tobytes(), 0, []
+    for e in ref.tolist():
+        want.append(hashlib.new("sha512_256", raw[s:e]).hexdigest())
+        s = e
+    assert ids == want
+    # one scan per piece per rank: the re-walk of the zero-run seam re-ran
+    # only the stitch over the kept candidate lists
+    assert all(x[2] == 1 for x in out)
+
+
+def test_bench_two_ranks_gloo_check():
+    """bench.py --gpus 2 --check through torch.distributed.run (DeviceShard,
+    HBM seam records, gloo staging): the sharded cut list equals one
+    dsx_cut_device over the whole blob."""
+    env = dict(os.environ, DSX_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--gib", "0.25", "--check", "--no-cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "check ok" in r.stderr, r.stderr[-2000:]
+    assert '"n_gpus": 2' in r.stdout

@@ -558,6 +558,7 @@ def _shard_protocol(data, world, dev):
                                      ctypes.c_void_p(ptr[r]), sflag), ctxs[r].h)
     outs = [np.empty(length // MIN + 4 + 1024, np.uint64) for _, length in geo]
     counts = [ctypes.c_uint64() for _ in range(world)]
+    pieces = [c.stats().pieces for c in ctxs]
     rounds = 0
     while True:
         rounds += 1
@@ -577,6 +578,8 @@ def _shard_protocol(data, world, dev):
         assert all(rc == _lib.DSX_E_RESYNC for rc in rcs), rcs
     got = np.concatenate([outs[r][:counts[r].value] for r in range(world)])
     assert np.array_equal(got, o.chunk_stream(data, MIN, AVG, MAX))
+    # a re-walk re-runs only the stitch over the kept candidate lists
+    assert [c.stats().pieces for c in ctxs] == pieces
     for c in ctxs:
         c.close()
     return rounds

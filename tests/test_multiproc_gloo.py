@@ -1,8 +1,11 @@
-"""N>1 path on CPU: world_size-2 "gloo" processes run the seam protocol of
-desync_amd.shard (fixed-size dsx_seam_t records, all-gathered) with the CPU
-restatement of dsx_shard_local / dsx_shard_resolve (oracle/seam.py), and the
-concatenated per-rank cut lists must equal the sequential chunker
-(make_test.go:16-80's property, across processes)."""
+"""N>1 path on CPU: world_size 2 and 3 "gloo" processes run desync_amd.shard's
+seam_protocol -- the exchange / resolve / re-walk loop every transport of
+the product shares -- with an engine that restates the two library calls on
+the CPU (oracle/seam.py).  The concatenated per-rank cut lists must equal the
+sequential chunker (make_test.go:16-80's property, across processes), and a
+rank that fails mid-protocol must make every rank fail instead of hanging
+(ADVICE r1).  The same loop over libdsx runs on the GPU in
+tests/test_gpu_multiproc.py."""
 import os
 import socket
 
@@ -43,36 +46,81 @@ def _from_struct(S):
                 cuts=[S.cuts[i] for i in range(S.ncuts)])
 
 
-def _worker(rank, world, port, data, result_q):
+class OracleEngine:
+    """seam_protocol's engine interface with dsx_shard_local / resolve
+    restated on the CPU (oracle/seam.py); records are the dsx_seam_t bytes
+    the library exchanges."""
+
+    def __init__(self, data, rank, world, fail_at=None):
+        from desync_amd import shard
+        self.sh = shard
+        self.data, self.rank, self.world = data, rank, world
+        total = data.size
+        span = total // world
+        self.start = rank * span
+        self.length = span if rank < world - 1 else total - self.start
+        self.fail_at = fail_at
+        self.rounds = 0
+
+    def local(self):
+        from oracle import seam as oseam
+        self.rec, self.spec, self.cands = oseam.shard_local(self.data, self.start, self.length,
+                                                            self.data.size, MIN, AVG, MAX)
+        return self.sh.seam_to_bytes(_to_struct(self.rec))
+
+    def exchange(self, rec):
+        return self.sh.exchange_seams(rec)
+
+    def failed(self, allb):
+        return self.sh.failed_ranks(allb, self.world)
+
+    def resolve(self, allb):
+        from oracle import seam as oseam
+        self.rounds += 1
+        if self.fail_at == self.rounds:
+            raise IOError("injected failure")
+        seams = [_from_struct(s) for s in self.sh.seams_from_bytes(allb, self.world)]
+        st, a, b = oseam.resolve(seams, self.rank, MIN, MAX)
+        if st == "ok":
+            self.mine = oseam.rank_cuts(a, b, self.spec)
+            return "ok"
+        if a == self.rank:  # this rank's seam did not converge: re-walk from the true entry
+            self.rec, self.spec = oseam.rewalk(self.cands, b, self.start, self.length,
+                                               self.data.size, MIN, MAX)
+        return "resync"
+
+    def record(self):
+        return self.sh.seam_to_bytes(_to_struct(self.rec))
+
+    def mark_error(self, rec):
+        from desync_amd import _lib
+        b = bytearray(rec)
+        off = self.sh.FLAGS_OFF
+        b[off:off + 4] = (int.from_bytes(b[off:off + 4], "little") | _lib.DSX_SEAM_ERROR).to_bytes(4, "little")
+        return bytes(b)
+
+    def result(self):
+        return self.mine
+
+
+def _worker(rank, world, port, data, result_q, fail_rank):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch.distributed as dist
     from desync_amd import shard
-    from oracle import seam as oseam
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    total = data.size
-    span = total // world
-    start = rank * span
-    length = span if rank < world - 1 else total - start
-    rec, spec, cands = oseam.shard_local(data, start, length, total, MIN, AVG, MAX)
-    rounds = 0
-    while True:  # the DSX_E_RESYNC protocol of desync_amd.shard.shard_chunk
-        rounds += 1
-        assert rounds <= world + 1
-        allb = shard.exchange_seams(shard.seam_to_bytes(_to_struct(rec)))
-        seams = [_from_struct(s) for s in shard.seams_from_bytes(allb, world)]
-        assert seams[rank]["exit_cut"] == rec["exit_cut"]
-        st, a, b = oseam.resolve(seams, rank, MIN, MAX)
-        if st == "ok":
-            mine = oseam.rank_cuts(a, b, spec)
-            break
-        if a == rank:  # this rank's seam did not converge: re-walk from the true entry
-            rec, spec = oseam.rewalk(cands, b, start, length, total, MIN, MAX)
-    out = [None] * world
-    dist.all_gather_object(out, mine.tolist())
-    if rank == 0:
-        result_q.put((sum(out, []), rounds))
+    eng = OracleEngine(data, rank, world, fail_at=1 if rank == fail_rank else None)
+    try:
+        mine = shard.seam_protocol(eng, world)
+        out = [None] * world
+        dist.all_gather_object(out, mine.tolist())
+        if rank == 0:
+            result_q.put(("ok", sum(out, []), eng.rounds))
+    except shard.PeerFailed:
+        result_q.put(("peer", rank, None))
+    except IOError:
+        result_q.put(("own", rank, None))
     dist.destroy_process_group()
 
 
@@ -92,21 +140,37 @@ def _compose(kind):
     return np.concatenate([r1, null, null, null, r1, null, null, null, r2])
 
 
+def _run(data, world, fail_rank=None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, q, fail_rank))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(1 if fail_rank is None else world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return msgs
+
+
 @pytest.mark.parametrize("kind", ["random", "spread-null", "seam-zero-run"])
 @pytest.mark.parametrize("world", [2, 3])
 def test_seam_protocol_gloo(kind, world):
     from oracle import oracle as o
     data = _compose(kind)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    got, rounds = q.get(timeout=300)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    (st, got, rounds), = _run(data, world)
+    assert st == "ok"
     assert got == o.chunk_stream(data, MIN, AVG, MAX).tolist()
     if kind == "seam-zero-run":
         assert rounds > 1  # the re-walk path ran
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, 1), (3, 0), (3, 2)])
+def test_seam_protocol_failure_propagates(world, fail_rank):
+    """One rank's resolve fails: it publishes DSX_SEAM_ERROR in one more
+    exchange, every other rank raises PeerFailed; nobody hangs."""
+    msgs = _run(_compose("seam-zero-run"), world, fail_rank)
+    kinds = sorted((m[1], m[0]) for m in msgs)
+    assert kinds == [(r, "own" if r == fail_rank else "peer") for r in range(world)]
