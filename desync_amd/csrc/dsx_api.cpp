@@ -175,6 +175,11 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
+  if (const char* v = getenv("DSX_DMA_POLICY")) c->dma_policy = (uint32_t)atoi(v) & 3u;
+  if (const char* v = getenv("DSX_SCANM")) {
+    const int w = atoi(v);
+    c->scanm_waves = (w == 12 || w == 16) ? w : 0;
+  }
   if (const char* v = getenv("DSX_SCAN_TRACE")) c->scan_trace = atoi(v) != 0;
   if (const char* v = getenv("DSX_WAVE_MAJOR")) c->wave_major = atoi(v) != 0;
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
@@ -321,7 +326,9 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   // when the grid origin P - delta would precede position 0
   const uint32_t delta = (uint32_t)((uintptr_t)d_piece & (kLine - 1));
   const bool line = c->scan_line && !cc.dense && P >= delta;
-  const int W = line ? c->scanl_waves : kCfgWaves[c->scan_cfg];
+  const int W = line ? (c->scanm_waves ? c->scanm_waves : c->scanl_waves) : kCfgWaves[c->scan_cfg];
+  // warm-up row ahead of each lane segment: a 128-B line (scanl) or a 64-B row (scanm)
+  const uint32_t warm_row = line && c->scanm_waves ? 64u : (uint32_t)kLine;
   const int cfgBR = kCfgBR[c->scan_cfg];
   const uint64_t slots_total = (uint64_t)c->ncu * W;  // wave slots
   const uint64_t span = line ? len + delta : len;       // grid bytes
@@ -422,15 +429,16 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.queue_next = c->overflow.p + 2 + ((seq + 1) & 1);
   sa.state_init = c->init_pending ? (void*)c->state.p : nullptr;
   sa.wave_major = c->wave_major ? 1u : 0u;
+  sa.dma_policy = c->dma_policy;
   sa.init_carry = c->init_carry;
   if (line) {
     // region 0's descriptor: the warm-up line unless it would start before
     // the readable bytes (then the 16-B step at or below base - min(halo, 48))
     const uint64_t hmin = std::min<uint64_t>(halo, kRound);
     sa.delta = delta;
-    sa.shift0 = halo >= (uint64_t)delta + kLine
+    sa.shift0 = halo >= (uint64_t)delta + warm_row
                     ? 0u
-                    : (uint32_t)(16 * (((uint64_t)kLine + delta - hmin) / 16));
+                    : (uint32_t)(16 * (((uint64_t)warm_row + delta - hmin) / 16));
   }
   c->last_grid_P = line ? P - delta : P;
   if (c->scan_trace && line) {
@@ -477,6 +485,8 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
       hipLaunchKernelGGL((scanl_kernel<2, 4, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (c->variant == 5)                                                             \
       hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D>), g, b, 0, c->stream, sa);       \
+    else if (c->variant == 6 && mode == 2)                                                \
+      hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (mode == 2)                                                                   \
       hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (mode == 1)                                                                   \
@@ -484,7 +494,22 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     else                                                                                  \
       hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
   } while (0)
-    if (line) {
+#define DSX_LAUNCHM(WV)                                                                   \
+  do {                                                                                    \
+    if (c->variant == 5)                                                                  \
+      hipLaunchKernelGGL((scanm_kernel<2, 5, WV>), g, b, 0, c->stream, sa);               \
+    else if (mode == 2)                                                                   \
+      hipLaunchKernelGGL((scanm_kernel<2, 0, WV>), g, b, 0, c->stream, sa);               \
+    else if (mode == 1)                                                                   \
+      hipLaunchKernelGGL((scanm_kernel<1, 0, WV>), g, b, 0, c->stream, sa);               \
+    else                                                                                  \
+      hipLaunchKernelGGL((scanm_kernel<0, 0, WV>), g, b, 0, c->stream, sa);               \
+  } while (0)
+    if (line && c->scanm_waves == 16) {
+      DSX_LAUNCHM(16);
+    } else if (line && c->scanm_waves == 12) {
+      DSX_LAUNCHM(12);
+    } else if (line) {
       DSX_LAUNCHL(8, 8, 1);
     } else switch (c->scan_cfg) {
       case 1: DSX_LAUNCH(1, 2, 12, 4, false); break;
@@ -498,6 +523,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     }
 #undef DSX_LAUNCH
 #undef DSX_LAUNCHL
+#undef DSX_LAUNCHM
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));

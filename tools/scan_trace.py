@@ -39,10 +39,13 @@ tr = tr[tr[:, 1] > 0]
 if os.environ.get("DSX_SCAN_VARIANT") == "5":
     # shader-clock cycles per wave and cycles spent waiting for the line DMA
     tot = (tr[:, 1] - tr[:, 0]).astype(np.float64)
-    frac = tr[:, 2] / tot
+    m = (1 << 21) - 1
+    parts = {"vmcnt wait": tr[:, 2] & m, "line copy + lgkmcnt(0)": (tr[:, 2] >> 21) & m,
+             "DMA issue": (tr[:, 2] >> 42) & m}
     q = [0, 10, 50, 90, 100]
-    print(f"waves {len(tr)}  DMA-wait fraction pct {q} {np.percentile(frac, q).round(3).tolist()}")
-    print(f"  cycles per wave median {np.median(tot):.0f}, waiting median {np.median(tr[:, 2]):.0f}")
+    print(f"waves {len(tr)}  cycles per wave median {np.median(tot):.0f}")
+    for k, v in parts.items():
+        print(f"  {k:24s} fraction pct {q} {np.percentile(v / tot, q).round(4).tolist()}")
     sys.exit(0)
 t0 = tr[:, 0].min()
 st = (tr[:, 0] - t0) / 100.0  # us (100 MHz)
