@@ -120,6 +120,13 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                 "(make -C desync_amd/csrc). desync_amd has no CPU fallback.")
+        diag_env = [k for k in ("DSX_SCAN_VARIANT", "DSX_SCAN_CFG")
+                    if os.environ.get(k, "0") not in ("", "0")]
+        if diag_env and not os.path.basename(LIB_PATH).startswith("libdsx_diag"):
+            raise ImportError(
+                f"{', '.join(diag_env)} selects a diagnostic scan kernel, which only the "
+                "diagnostic build holds: make -C desync_amd/csrc diag and set "
+                "DSX_LIB_PATH=desync_amd/libdsx_diag.so")
         _share_torch_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         u64, u32, i32, vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p

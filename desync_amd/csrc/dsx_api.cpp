@@ -170,16 +170,13 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   CREATE_STEP(hipGetDeviceProperties(&prop, device));
   c->ncu = prop.multiProcessorCount;
   if (const char* m = getenv("DSX_TEST_MODE")) c->force_mode = atoi(m);
+#if DSX_DIAG  // ablation variants and alternative geometries: libdsx_diag.so only
   if (const char* v = getenv("DSX_SCAN_VARIANT")) c->variant = atoi(v);
+  if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
+#endif
   if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
-  if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
-  if (const char* v = getenv("DSX_DMA_POLICY")) c->dma_policy = (uint32_t)atoi(v) & 3u;
-  if (const char* v = getenv("DSX_SCANM")) {
-    const int w = atoi(v);
-    c->scanm_waves = (w == 12 || w == 16) ? w : 0;
-  }
   if (const char* v = getenv("DSX_SCAN_TRACE")) c->scan_trace = atoi(v) != 0;
   if (const char* v = getenv("DSX_WAVE_MAJOR")) c->wave_major = atoi(v) != 0;
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
@@ -326,9 +323,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   // when the grid origin P - delta would precede position 0
   const uint32_t delta = (uint32_t)((uintptr_t)d_piece & (kLine - 1));
   const bool line = c->scan_line && !cc.dense && P >= delta;
-  const int W = line ? (c->scanm_waves ? c->scanm_waves : c->scanl_waves) : kCfgWaves[c->scan_cfg];
-  // warm-up row ahead of each lane segment: a 128-B line (scanl) or a 64-B row (scanm)
-  const uint32_t warm_row = line && c->scanm_waves ? 64u : (uint32_t)kLine;
+  const int W = line ? c->scanl_waves : kCfgWaves[c->scan_cfg];
   const int cfgBR = kCfgBR[c->scan_cfg];
   const uint64_t slots_total = (uint64_t)c->ncu * W;  // wave slots
   const uint64_t span = line ? len + delta : len;       // grid bytes
@@ -429,16 +424,15 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.queue_next = c->overflow.p + 2 + ((seq + 1) & 1);
   sa.state_init = c->init_pending ? (void*)c->state.p : nullptr;
   sa.wave_major = c->wave_major ? 1u : 0u;
-  sa.dma_policy = c->dma_policy;
   sa.init_carry = c->init_carry;
   if (line) {
     // region 0's descriptor: the warm-up line unless it would start before
     // the readable bytes (then the 16-B step at or below base - min(halo, 48))
     const uint64_t hmin = std::min<uint64_t>(halo, kRound);
     sa.delta = delta;
-    sa.shift0 = halo >= (uint64_t)delta + warm_row
+    sa.shift0 = halo >= (uint64_t)delta + kLine
                     ? 0u
-                    : (uint32_t)(16 * (((uint64_t)warm_row + delta - hmin) / 16));
+                    : (uint32_t)(16 * (((uint64_t)kLine + delta - hmin) / 16));
   }
   c->last_grid_P = line ? P - delta : P;
   if (c->scan_trace && line) {
@@ -460,70 +454,68 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)c->ncu);
     const dim3 g(grid), b(W * kWave);
     const int mode = pick_mode(c, p->discriminator);
+#if DSX_DIAG
+#define DSX_ABLATE(K, ...)                                                                 \
+  if (c->variant == 1) hipLaunchKernelGGL((K<2, 1, __VA_ARGS__>), g, b, 0, c->stream, sa); \
+  else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__>), g, b, 0, c->stream, sa); \
+  else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__>), g, b, 0, c->stream, sa); \
+  else
+#else
+#define DSX_ABLATE(K, ...)
+#endif
 #define DSX_LAUNCH(BR, NB, WV, SUB, PF)                                                    \
   do {                                                                                     \
-    if (c->variant == 1)                                                                   \
-      hipLaunchKernelGGL((scan_kernel<2, 1, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
-    else if (c->variant == 3)                                                              \
-      hipLaunchKernelGGL((scan_kernel<2, 3, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
-    else if (c->variant == 4)                                                              \
-      hipLaunchKernelGGL((scan_kernel<2, 4, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
-    else if (mode == 2)                                                                    \
+    DSX_ABLATE(scan_kernel, BR, NB, WV, SUB, PF)                                           \
+    if (mode == 2)                                                                         \
       hipLaunchKernelGGL((scan_kernel<2, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
     else if (mode == 1)                                                                    \
       hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
     else                                                                                   \
       hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
   } while (0)
+#if DSX_DIAG
+#define DSX_TRACE_VARIANTS(WV, SUB, D)                                                    \
+  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D>), g, b, 0, c->stream, sa); \
+  else if (c->variant == 6 && mode == 2)                                                  \
+    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D>), g, b, 0, c->stream, sa);         \
+  else
+#else
+#define DSX_TRACE_VARIANTS(WV, SUB, D)
+#endif
 #define DSX_LAUNCHL(WV, SUB, D)                                                           \
   do {                                                                                    \
-    if (c->variant == 1)                                                                  \
-      hipLaunchKernelGGL((scanl_kernel<2, 1, WV, SUB, D>), g, b, 0, c->stream, sa);       \
-    else if (c->variant == 3)                                                             \
-      hipLaunchKernelGGL((scanl_kernel<2, 3, WV, SUB, D>), g, b, 0, c->stream, sa);       \
-    else if (c->variant == 4)                                                             \
-      hipLaunchKernelGGL((scanl_kernel<2, 4, WV, SUB, D>), g, b, 0, c->stream, sa);       \
-    else if (c->variant == 5)                                                             \
-      hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D>), g, b, 0, c->stream, sa);       \
-    else if (c->variant == 6 && mode == 2)                                                \
-      hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D>), g, b, 0, c->stream, sa);       \
-    else if (mode == 2)                                                                   \
+    DSX_ABLATE(scanl_kernel, WV, SUB, D)                                                  \
+    DSX_TRACE_VARIANTS(WV, SUB, D)                                                        \
+    if (mode == 2)                                                                        \
       hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else if (mode == 1)                                                                   \
       hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
     else                                                                                  \
       hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
   } while (0)
-#define DSX_LAUNCHM(WV)                                                                   \
-  do {                                                                                    \
-    if (c->variant == 5)                                                                  \
-      hipLaunchKernelGGL((scanm_kernel<2, 5, WV>), g, b, 0, c->stream, sa);               \
-    else if (mode == 2)                                                                   \
-      hipLaunchKernelGGL((scanm_kernel<2, 0, WV>), g, b, 0, c->stream, sa);               \
-    else if (mode == 1)                                                                   \
-      hipLaunchKernelGGL((scanm_kernel<1, 0, WV>), g, b, 0, c->stream, sa);               \
-    else                                                                                  \
-      hipLaunchKernelGGL((scanm_kernel<0, 0, WV>), g, b, 0, c->stream, sa);               \
-  } while (0)
-    if (line && c->scanm_waves == 16) {
-      DSX_LAUNCHM(16);
-    } else if (line && c->scanm_waves == 12) {
-      DSX_LAUNCHM(12);
-    } else if (line) {
+    if (line) {
       DSX_LAUNCHL(8, 8, 1);
-    } else switch (c->scan_cfg) {
-      case 1: DSX_LAUNCH(1, 2, 12, 4, false); break;
-      case 2: DSX_LAUNCH(1, 2, 16, 4, false); break;
-      case 3: DSX_LAUNCH(2, 1, 12, 8, false); break;
-      case 4: DSX_LAUNCH(2, 1, 8, 8, false); break;
-      case 5: DSX_LAUNCH(2, 1, 16, 4, false); break;
-      default:
-        if (c->prefetch_batches > 0) DSX_LAUNCH(2, 2, 8, 8, true);
-        else DSX_LAUNCH(2, 2, 8, 8, false);
+    } else {
+#if DSX_DIAG
+      switch (c->scan_cfg) {
+        case 1: DSX_LAUNCH(1, 2, 12, 4, false); break;
+        case 2: DSX_LAUNCH(1, 2, 16, 4, false); break;
+        case 3: DSX_LAUNCH(2, 1, 12, 8, false); break;
+        case 4: DSX_LAUNCH(2, 1, 8, 8, false); break;
+        case 5: DSX_LAUNCH(2, 1, 16, 4, false); break;
+        default:
+          if (c->prefetch_batches > 0) DSX_LAUNCH(2, 2, 8, 8, true);
+          else DSX_LAUNCH(2, 2, 8, 8, false);
+      }
+#else
+      if (c->prefetch_batches > 0) DSX_LAUNCH(2, 2, 8, 8, true);
+      else DSX_LAUNCH(2, 2, 8, 8, false);
+#endif
     }
 #undef DSX_LAUNCH
 #undef DSX_LAUNCHL
-#undef DSX_LAUNCHM
+#undef DSX_ABLATE
+#undef DSX_TRACE_VARIANTS
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));

@@ -72,7 +72,6 @@ struct ScanArgs {
   uint32_t shift0;
   uint64_t* trace;       // diagnostics (DSX_SCAN_TRACE): per wave slot {start, end, regions}
   uint32_t wave_major;   // first regions wave-major over the grid (DSX_WAVE_MAJOR, default 1)
-  uint32_t dma_policy;   // cache policy of the line DMA: 0 default, 1 nt, 2 sc1, 3 sc0 sc1 nt (DSX_DMA_POLICY)
   uint32_t pad_;
 };
 

@@ -22,8 +22,6 @@ template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ void scan_kernel(ScanArgs a);
 template <int MODE, int VARIANT, int W, int SUB, int D>
 __global__ void scanl_kernel(ScanArgs a);
-template <int MODE, int VARIANT, int W>
-__global__ void scanm_kernel(ScanArgs a);
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);
@@ -103,8 +101,6 @@ struct dsx_ctx {
   int scan_cfg = 0;                   // DSX_SCAN_CFG: index into kCfg* (waves, rounds/batch, LDS buffers)
   bool scan_line = true;              // DSX_SCAN_LINE=0: 96-B-row scan_kernel instead of scanl_kernel
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
-  uint32_t dma_policy = 0;            // DSX_DMA_POLICY: cache policy bits of the scan's line DMA
-  int scanm_waves = 0;                // DSX_SCANM=12|16: scanm_kernel (64-B rows) with that many waves
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
   uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR

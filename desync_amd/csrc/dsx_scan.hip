@@ -55,35 +55,17 @@ __constant__ uint32_t kT[256] = DSX_BUZHASH_TABLE_INIT;
 // hipcc does not treat later ds_reads as aliasing a pending DMA (it would
 // drain vmcnt(0) in front of unrelated LDS reads); completion is tracked by
 // the explicit s_waitcnt vmcnt(0) before a batch is read.
-template <int POL>
-__device__ __forceinline__ void dma16p(const u32x4& rsrc, uint32_t voff, uint32_t lds_addr) {
-  uint32_t keep;
-#define DSX_DMA16_ASM(MOD)                                      \
-  asm volatile(                                                 \
-      "s_mov_b32 %0, m0\n\t"                                    \
-      "s_mov_b32 m0, %2\n\t"                                    \
-      "s_nop 0\n\t"                                             \
-      "buffer_load_dwordx4 %1, %3, 0 offen" MOD " lds\n\t"      \
-      "s_mov_b32 m0, %0"                                        \
-      : "=&s"(keep)                                             \
-      : "v"(voff), "s"(lds_addr), "s"(rsrc)                     \
-      : "memory")
-  if constexpr (POL == 1) DSX_DMA16_ASM(" nt");
-  else if constexpr (POL == 2) DSX_DMA16_ASM(" sc1");
-  else if constexpr (POL == 3) DSX_DMA16_ASM(" sc0 sc1 nt");
-  else DSX_DMA16_ASM("");
-#undef DSX_DMA16_ASM
-}
 __device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t lds_addr) {
-  dma16p<0>(rsrc, voff, lds_addr);
-}
-// the policy is uniform per launch: a scalar branch per DMA instruction
-__device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t lds_addr,
-                                      uint32_t pol) {
-  if (pol == 0) dma16p<0>(rsrc, voff, lds_addr);
-  else if (pol == 1) dma16p<1>(rsrc, voff, lds_addr);
-  else if (pol == 2) dma16p<2>(rsrc, voff, lds_addr);
-  else dma16p<3>(rsrc, voff, lds_addr);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds_addr), "s"(rsrc)
+      : "memory");
 }
 
 // L2 prefetch: one dword per lane (buffer_load_dword ... lds) into the first
@@ -535,20 +517,29 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the trailing zero loads
 }
 
+// The product library holds the results-exact kernels (VARIANT 0) of the
+// default configurations; the diagnostic build (make diag -> libdsx_diag.so,
+// -DDSX_DIAG=1, loaded through DSX_LIB_PATH by tools/) adds the ablations and
+// the other geometries.
 #define DSX_SCAN_INST(BR, NBUF, W, SUB, PF)                                   \
   template __global__ void scan_kernel<0, 0, BR, NBUF, W, SUB, PF>(ScanArgs); \
   template __global__ void scan_kernel<1, 0, BR, NBUF, W, SUB, PF>(ScanArgs); \
-  template __global__ void scan_kernel<2, 0, BR, NBUF, W, SUB, PF>(ScanArgs); \
+  template __global__ void scan_kernel<2, 0, BR, NBUF, W, SUB, PF>(ScanArgs);
+#define DSX_SCAN_INST_DIAG(BR, NBUF, W, SUB, PF)                              \
   template __global__ void scan_kernel<2, 1, BR, NBUF, W, SUB, PF>(ScanArgs); \
   template __global__ void scan_kernel<2, 3, BR, NBUF, W, SUB, PF>(ScanArgs); \
   template __global__ void scan_kernel<2, 4, BR, NBUF, W, SUB, PF>(ScanArgs);
 DSX_SCAN_INST(2, 2, 8, 8, false)
 DSX_SCAN_INST(2, 2, 8, 8, true)
+#if DSX_DIAG
+DSX_SCAN_INST_DIAG(2, 2, 8, 8, false)
+DSX_SCAN_INST_DIAG(2, 2, 8, 8, true)
 DSX_SCAN_INST(1, 2, 12, 4, false)
 DSX_SCAN_INST(1, 2, 16, 4, false)
 DSX_SCAN_INST(2, 1, 12, 8, false)
 DSX_SCAN_INST(2, 1, 8, 8, false)
 DSX_SCAN_INST(2, 1, 16, 4, false)
+#endif
 
 // ---------------------------------------------------------------------------
 // scanl_kernel -- the line-aligned scan (default path).
@@ -631,7 +622,6 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   const uint32_t stage_lds =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)stage);
   const uint32_t S = a.lane_bytes;
-  const uint32_t pol = __builtin_amdgcn_readfirstlane(a.dma_policy);
   const uint32_t M = a.batches;        // loop trips of 3 batches: S = 3*128*M
   const uint32_t NB = 3u * M + 1u;     // batches per lane, warm-up line included
   const uint64_t RB = 64ull * S;
@@ -677,7 +667,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       uint32_t ssum = (uint32_t)i * 8u * S + sb;
       asm volatile("" : "+s"(ssum));
       const uint32_t vo = (b < NB) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
-      dma16(rsrc, vo, stage_lds + (uint32_t)i * 1024u, pol);
+      dma16(rsrc, vo, stage_lds + (uint32_t)i * 1024u);
     }
   };
 
@@ -979,381 +969,15 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 #define DSX_SCANL_INST(W, SUB, D)                                       \
   template __global__ void scanl_kernel<0, 0, W, SUB, D>(ScanArgs);     \
   template __global__ void scanl_kernel<1, 0, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 0, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 1, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 3, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 4, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 5, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 6, W, SUB, D>(ScanArgs);
+  template __global__ void scanl_kernel<2, 0, W, SUB, D>(ScanArgs);
+#if DSX_DIAG
+template __global__ void scanl_kernel<2, 1, 8, 8, 1>(ScanArgs);
+template __global__ void scanl_kernel<2, 3, 8, 8, 1>(ScanArgs);
+template __global__ void scanl_kernel<2, 4, 8, 8, 1>(ScanArgs);
+template __global__ void scanl_kernel<2, 5, 8, 8, 1>(ScanArgs);
+template __global__ void scanl_kernel<2, 6, 8, 8, 1>(ScanArgs);
+#endif
 DSX_SCANL_INST(8, 8, 1)  // D = 2 needs 16 more VGPRs than the 256 of two waves per SIMD
-
-// ---------------------------------------------------------------------------
-// scanm_kernel -- the scan with more waves per SIMD.
-//
-// Why: a wave alone issues one VALU instruction every ~5.5 cycles whatever its
-// type (tools/ubench_valu.hip, wps=1), while the slow integer ops of the hash
-// (v_perm, v_alignbit, v_bitop3, v_mul_lo, v_min3) take ~4.6 cycles of the
-// SIMD; with two waves per SIMD (scanl_kernel, 243 VGPRs) the SIMD is idle
-// whenever either wave is in its line fetch (10 % of a wave: DMA issue 7.5 %,
-// line copy 2 %) or waits for lookups: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
-// showed the VALU 69 % busy.  This kernel fits W/4 = 3 or 4 waves per SIMD:
-//   * rows of 64 B per lane (half a line; the L2 serves the other half of a
-//     line the DMA fetched one row earlier): 4 KiB of staging per wave, so
-//     16 waves fit beside the 64 KiB table;
-//   * the row in 16 VGPRs, one lookup buffer of 8 entries refilled byte by
-//     byte right after each entry is consumed (lookups run one subgroup of 8
-//     bytes ahead), the 48-entry ring of outgoing terms.
-// Per byte the work is scanl_kernel's: one v_perm + ds_read_b64 lookup,
-// v_alignbit + v_bitop3 for the hash, one v_mul_lo_u32 for the boundary
-// prefilter, a v_min3 every two bytes.
-// Rows are stored rotated by (row >> 2) mod 4 chunks, which makes the
-// ds_read_b128 row copies bank-conflict-free (each 16-lane group covers the
-// 16 bank quads).  A trip is 6 rows = 384 B = 8 windows (static ring slots).
-// ---------------------------------------------------------------------------
-template <int MODE, int VARIANT, int W>
-__global__ __launch_bounds__(W * kWave, W / 4) void scanm_kernel(ScanArgs a) {
-  constexpr int kRow = 64;                   // bytes per lane row
-  constexpr int NC = kRow / 16;              // 16-B chunks per row
-  constexpr int NI = kWave * kRow / 1024;    // DMA wave instructions per row batch
-  constexpr int STG = kWave * kRow;          // staging bytes per wave
-  constexpr int LDSB = kTableBytes + W * STG;
-  constexpr int NT = W * kWave;
-  constexpr bool kBal = LDSB + 4 * W <= kScanLds;
-  static_assert(LDSB <= kScanLds, "LDS budget");
-  static_assert(NC == 4 && NI == 4, "row DMA geometry");
-  // the kernel's only LDS variable, so the table sits at LDS address 0 and a
-  // v_perm result is a complete lookup address (checked below)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB + (kBal ? 4 * W : 0)];
-  uint32_t* s_prog = reinterpret_cast<uint32_t*>(lds + LDSB);
-
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *a.overflow_next = 0u;
-    *a.queue_next = 0u;
-    if (a.state_init) {
-      uint64_t* st = (uint64_t*)a.state_init;
-      st[0] = a.init_carry;
-      st[1] = 0;
-      st[2] = 0;
-      st[3] = 0;
-      st[4] = 0;
-      st[5] = 0;
-    }
-  }
-  {  // the table: row v (256 B) = T[v] in 32 lane slots, then rotl16(T[v]) in
-     // 32 lane slots: two conflict-free ds_read_b32 per lookup whose results
-     // are single registers (the outgoing term lives 48 bytes in the ring;
-     // a 64-bit {T, Trot} pair would keep its dead half alive as long)
-    static_assert(NT % 256 == 0, "table fill shape");
-    constexpr int TPV = NT / 256;
-    const uint32_t v = threadIdx.x & 255u;
-    const uint32_t tv = kT[v];
-    const uint32_t tr = __builtin_amdgcn_alignbit(tv, tv, 16);
-#pragma unroll
-    for (int k = 0; k < (32 + TPV - 1) / TPV; ++k) {
-      const uint32_t slot = (threadIdx.x >> 8) + (uint32_t)(k * TPV);
-      if (slot < 32u) {
-        *reinterpret_cast<uint32_t*>(lds + v * 256u + slot * 4u) = tv;
-        *reinterpret_cast<uint32_t*>(lds + v * 256u + 128u + slot * 4u) = tr;
-      }
-    }
-  }
-  if (kBal && threadIdx.x < W) s_prog[threadIdx.x] = 0u;
-  __syncthreads();
-
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t slot4 = (lane & 31u) * 4u;
-  uint8_t* stage = lds + kTableBytes + wave * STG;
-  // waves w, w + W/4, w + W/2, ... share a SIMD; the one furthest behind the
-  // next wave of its SIMD takes issue priority (as in scanl_kernel)
-  const uint32_t partner = (wave + (uint32_t)W / 4u) % (uint32_t)W;
-  uint32_t my_prog = 0;
-  const uint32_t stage_lds =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)stage);
-  if (stage_lds != (uint32_t)kTableBytes + wave * (uint32_t)STG) {
-    if (threadIdx.x == 0) atomicAdd(a.overflow, 0x40000000u);  // never: results rejected
-    return;
-  }
-  const uint32_t S = a.lane_bytes;
-  const uint32_t M = a.batches;        // trips of 6 rows: S = 384*M
-  const uint32_t NB = 6u * M + 1u;     // row batches per lane, warm-up row included
-  const uint64_t RB = 64ull * S;
-  // DMA: instruction i, lane j -> 16-B unit u = 64i + j: row u/4 =
-  // 16i + j/4, physical chunk j%4 holding logical chunk (j - rot) % 4 with
-  // rot(row) = (row >> 2) % 4 = (j >> 4) % 4 (independent of i)
-  const uint32_t dbase = (lane >> 2) * S + (((lane & 3u) + 4u - ((lane >> 4) & 3u)) & 3u) * 16u;
-  const uint32_t rot = (lane >> 2) & 3u;
-  TestConsts tcv = a.tc;
-
-  auto desc_of = [&](uint32_t region, u32x4& rsrc, uint32_t& sh) {
-    sh = region == 0 ? a.shift0 : 0u;
-    const int64_t rel = (int64_t)region * (int64_t)RB - (int64_t)a.delta - kRow + (int64_t)sh;
-    const uint64_t rp = (uint64_t)(uintptr_t)(a.base + rel);
-    const uint64_t nrec64 = (uint64_t)((int64_t)a.len - rel);
-    const uint32_t nrec = nrec64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nrec64;
-    rsrc.x = __builtin_amdgcn_readfirstlane((uint32_t)rp);
-    rsrc.y = __builtin_amdgcn_readfirstlane((uint32_t)(rp >> 32) & 0xFFFFu);
-    rsrc.z = __builtin_amdgcn_readfirstlane(nrec);
-    rsrc.w = 0x00020000u;
-  };
-  auto issue = [&](const u32x4& rsrc, uint32_t sh, uint32_t b) {
-    const uint32_t sb = b * (uint32_t)kRow - sh;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      uint32_t ssum = (uint32_t)i * 16u * S + sb;
-      asm volatile("" : "+s"(ssum));
-      const uint32_t vo = (b < NB) ? dbase + ssum : 0xFFFFFFF0u;
-      dma16(rsrc, vo, stage_lds + (uint32_t)i * 1024u);
-    }
-  };
-
-  uint32_t region = a.wave_major ? wave * gridDim.x + blockIdx.x : blockIdx.x * W + wave;
-  if (region >= a.nregions) return;
-  const uint64_t t_start = VARIANT == 5 ? __builtin_amdgcn_s_memtime()
-                                        : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
-  uint64_t vm_wait = 0, copy_wait = 0, dma_issue = 0;
-  uint32_t nreg_done = 0;
-  u32x4 rsrc;
-  uint32_t sh;
-  desc_of(region, rsrc, sh);
-  uint32_t ticket = 0;
-  if (lane == 0) ticket = atomicAdd(a.queue, 1u);
-  issue(rsrc, sh, 0u);
-
-  while (true) {
-    const uint32_t next = gridDim.x * W + __builtin_amdgcn_readfirstlane(ticket);
-    u32x4 nrsrc = rsrc;
-    uint32_t nsh = 0;
-    if (next < a.nregions) {
-      if (lane == 0) ticket = atomicAdd(a.queue, 1u);
-      desc_of(next, nrsrc, nsh);
-    }
-
-    uint32_t cnt = 0;
-    uint32_t ereg[kHitRegs] = {};
-    const uint64_t gl = (uint64_t)region * 64u + lane;
-    uint32_t* myslots = a.lane_slot + gl * a.lane_slots;
-    uint32_t h = MODE == 2 ? ~0u : 0u;  // MODE 2 keeps ~h (see scanl_kernel)
-    uint32_t ring[48];
-#pragma unroll
-    for (int k = 0; k < 48; ++k) ring[k] = 0;
-    uint32_t w[NC * 4];
-
-    // wait for row batch b, copy this lane's row to registers, issue batch
-    // b+1 (or the next region's warm-up row) into the freed staging row
-    auto fetch = [&](uint32_t b) __attribute__((always_inline)) {
-      uint64_t tw = 0, tw1 = 0, tw2 = 0;
-      if constexpr (VARIANT == 5) tw = __builtin_amdgcn_s_memtime();
-      ++my_prog;
-      uint32_t their = my_prog;
-      if constexpr (kBal) {
-        s_prog[wave] = my_prog;
-        their = s_prog[partner];
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (VARIANT == 5) {
-        tw1 = __builtin_amdgcn_s_memtime();
-        vm_wait += tw1 - tw;
-      }
-      const uint8_t* my_row = stage + lane * (uint32_t)kRow;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const uint32_t pc = ((uint32_t)c + rot) & 3u;
-        const uint4 q = *reinterpret_cast<const uint4*>(my_row + pc * 16u);
-        w[4 * c] = q.x;
-        w[4 * c + 1] = q.y;
-        w[4 * c + 2] = q.z;
-        w[4 * c + 3] = q.w;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if constexpr (VARIANT == 5) {
-        tw2 = __builtin_amdgcn_s_memtime();
-        copy_wait += tw2 - tw1;
-      }
-      if (__builtin_amdgcn_readfirstlane(their) < my_prog)
-        __builtin_amdgcn_s_setprio(0);
-      else
-        __builtin_amdgcn_s_setprio(1);
-      if (b + 1u < NB)
-        issue(rsrc, sh, b + 1u);
-      else
-        issue(nrsrc, nsh, next < a.nregions ? 0u : NB);
-      if constexpr (VARIANT == 5) dma_issue += __builtin_amdgcn_s_memtime() - tw2;
-    };
-    // lookup of byte k of the row in w: T[b] and rotl16(T[b]) as two
-    // ds_read_b32 written here rather than by the compiler, which would merge
-    // them into one ds_read2_b32 whose register pair keeps T's dead half
-    // alive for the 48 bytes rotl16(T) spends in the ring.  The compiler does
-    // not count these reads: consume() waits for them explicitly.
-    auto lookup = [&](auto kc, uint32_t& tt, uint32_t& tr) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value;
-      const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8);
-      const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot4, sel);
-      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:128"
-                   : "=&v"(tt), "=v"(tr)
-                   : "v"(addr)
-                   : "memory");
-    };
-    auto wait_all = [&](uint32_t& tt, uint32_t& tr) __attribute__((always_inline)) {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tt), "+v"(tr));
-    };
-    // the lookup consumed now was issued 7 lookups (14 reads) before the
-    // newest; reads complete in order, so lgkmcnt <= 14 means it landed
-    auto consume_wait = [&](uint32_t& tt, uint32_t& tr) __attribute__((always_inline)) {
-      asm volatile("s_waitcnt lgkmcnt(14)" : "+v"(tt), "+v"(tr));
-    };
-    fetch(0u);
-    // warm-up: the last 48 bytes before the segment (bytes 16..63 of the
-    // warm-up row) fill the window, no test
-    static_for<6>([&](auto jc) __attribute__((always_inline)) {
-      constexpr int j = decltype(jc)::value;
-      uint32_t tt[8], tr[8];
-      static_for<8>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        lookup(std::integral_constant<int, 16 + j * 8 + q>{}, tt[q], tr[q]);
-      });
-      static_for<8>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        wait_all(tt[q], tr[q]);
-      });
-      static_for<8>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        constexpr int rk = j * 8 + q;
-        h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31), tt[q], ring[rk], 0x96);
-        ring[rk] = tr[q];
-      });
-    });
-    uint32_t LT[8], LR[8];  // lookups in flight: one subgroup ahead
-    // subgroup g (8 bytes) is hashed while the lookups of subgroup gi are
-    // issued, each right after the entry it replaces was consumed
-    auto step = [&](auto gc, auto gic, uint32_t o0) __attribute__((always_inline)) {
-      constexpr int g = decltype(gc)::value;
-      constexpr int gi = decltype(gic)::value;
-      uint32_t t[8];
-      static_for<8>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        constexpr int rk = (g * 8 + q) % 48;
-        consume_wait(LT[q], LR[q]);
-        h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31), LT[q], ring[rk],
-                                        0x96);
-        ring[rk] = LR[q];
-        lookup(std::integral_constant<int, (gi % 8) * 8 + q>{}, LT[q], LR[q]);
-        if constexpr (MODE == 2) t[q] = h * tcv.ninv;
-        else t[q] = is_cand<MODE>(h, tcv) ? 0u : 0xFFFFFFFFu;
-      });
-      const uint32_t thr = MODE == 2 ? tcv.vmax1 : 1u;
-      uint32_t mn = t[0];
-#pragma unroll
-      for (int q = 1; q < 8; ++q) mn = __builtin_elementwise_min(mn, t[q]);
-      if (__builtin_expect(__ballot(mn < thr) != 0, 0)) {
-        uint32_t bits = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          if constexpr (MODE == 2) bits |= (mode2_exact(t[q] - 1u, tcv) ? 1u : 0u) << q;
-          else bits |= (t[q] == 0u ? 1u : 0u) << q;
-        }
-        if (bits) {
-          const uint32_t e = (bits << 16) | (o0 + (uint32_t)(g * 8));
-#pragma unroll
-          for (int q = 0; q < kHitRegs; ++q) ereg[q] = cnt == (uint32_t)q ? e : ereg[q];
-          if (cnt >= (uint32_t)kHitRegs && cnt - kHitRegs < a.lane_slots)
-            myslots[cnt - kHitRegs] = e;
-          ++cnt;
-        }
-      }
-    };
-    fetch(1u);
-    static_for<8>([&](auto qc) __attribute__((always_inline)) {
-      constexpr int q = decltype(qc)::value;
-      lookup(std::integral_constant<int, q>{}, LT[q], LR[q]);
-    });
-    for (uint32_t t = 0; t < M; ++t) {
-      const uint32_t o0 = t * 6u * (uint32_t)kRow;
-      static_for<48>([&](auto gc) __attribute__((always_inline)) {
-        constexpr int g = decltype(gc)::value;
-        constexpr int gi = g + 1;  // subgroup whose lookups are issued now
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (gi < 48) {
-          if constexpr (gi % 8 == 0) fetch(6u * t + 1u + (uint32_t)(gi / 8));
-        } else {
-          if (t + 1 < M) fetch(6u * t + 7u);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // (on the last trip the final lookups read whatever the row holds:
-        // harmless, their results are never used)
-        step(gc, std::integral_constant<int, gi % 48>{}, o0);
-      });
-    }
-
-    // ---- region end: compact the lanes' hits into one sorted region list ----
-    const int64_t lane_p = (int64_t)region * (int64_t)RB + (int64_t)lane * S - (int64_t)a.delta;
-    int64_t lo = 1 - lane_p;
-    const int64_t lo2 = (int64_t)a.min_pos - (int64_t)a.piece_abs - lane_p;
-    lo = lo > lo2 ? lo : lo2;
-    const uint32_t o_min = lo <= 1 ? 1u : (lo > (int64_t)S ? S + 1u : (uint32_t)lo);
-    const int64_t hi = (int64_t)a.len - lane_p;
-    const uint32_t o_max = hi <= 0 ? 0u : (hi >= (int64_t)S ? S : (uint32_t)hi);
-    const uint32_t n = cnt < a.lane_slots + kHitRegs ? cnt : a.lane_slots + kHitRegs;
-    const bool spilled = __ballot(cnt > (uint32_t)kHitRegs) != 0;
-    auto for_each_hit = [&](auto&& f) {
-      auto expand = [&](uint32_t e) {
-        const uint32_t base = e & 0xFFFFu;
-        for (uint32_t bits = e >> 16; bits; bits &= bits - 1u) {
-          const uint32_t o = base + (uint32_t)__builtin_ctz(bits) + 1u;
-          if (o >= o_min && o <= o_max) f(o);
-        }
-      };
-#pragma unroll
-      for (int q = 0; q < kHitRegs; ++q)
-        if ((uint32_t)q < n) expand(ereg[q]);
-      if (spilled)
-        for (uint32_t i = kHitRegs; i < n; ++i) expand(myslots[i - kHitRegs]);
-    };
-    uint32_t keep = 0;
-    for_each_hit([&](uint32_t) { ++keep; });
-    uint32_t incl = keep;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t v = __shfl_up(incl, d, 64);
-      if (lane >= (uint32_t)d) incl += v;
-    }
-    const uint32_t excl = incl - keep;
-    uint32_t exact = keep;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) exact += __shfl_xor(exact, d, 64);
-    uint32_t* rl = a.region_list + (uint64_t)region * a.region_cap;
-    uint32_t j = 0;
-    for_each_hit([&](uint32_t o) {
-      if (excl + j < a.region_cap) rl[excl + j] = lane * S + o;
-      ++j;
-    });
-    const bool lane_ovf = __ballot(cnt > a.lane_slots + kHitRegs) != 0;
-    if (lane == 0) {
-      a.region_cnt[region] = exact;
-      if (lane_ovf || exact > a.region_cap) atomicAdd(a.overflow, 1u);
-    }
-    ++nreg_done;
-    if (next >= a.nregions) break;
-    region = next;
-    rsrc = nrsrc;
-    sh = nsh;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (a.trace && lane == 0) {
-    uint64_t* tr = a.trace + 3ull * (blockIdx.x * W + wave);
-    tr[0] = t_start;
-    tr[1] = VARIANT == 5 ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
-    tr[2] = VARIANT == 5 ? (vm_wait | (copy_wait << 21) | (dma_issue << 42)) : nreg_done;
-  }
-}
-
-#define DSX_SCANM_INST(W)                                          \
-  template __global__ void scanm_kernel<0, 0, W>(ScanArgs);        \
-  template __global__ void scanm_kernel<1, 0, W>(ScanArgs);        \
-  template __global__ void scanm_kernel<2, 0, W>(ScanArgs);        \
-  template __global__ void scanm_kernel<2, 5, W>(ScanArgs);
-DSX_SCANM_INST(16)
-DSX_SCANM_INST(12)
 
 // Exhaustive/ranged check of the GPU boundary predicate against h % d == d-1
 // (the plain form of chunker_test.go:190-213).  Diagnostic entry point.

@@ -234,8 +234,7 @@ def test_random_avg_sweep(dctx, avg):
 
 
 @pytest.mark.parametrize("env", [{"DSX_LANE_TARGET": "384"}, {"DSX_LANE_TARGET": "2304"},
-                                 {"DSX_SCAN_LINE": "0"}, {"DSX_SCAN_VARIANT": "0"},
-                                 {"DSX_SCANM": "16"}, {"DSX_SCANM": "12", "DSX_LANE_TARGET": "384"}])
+                                 {"DSX_SCAN_LINE": "0"}, {"DSX_WAVE_MAJOR": "0"}])
 def test_scan_geometries(env, monkeypatch):
     """The line-aligned scan with short lane segments (many regions per wave
     slot from the work queue), the 96-B-row scan_kernel, and device pointers
