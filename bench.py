@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--gib", type=float, default=1.0, help="GiB per GPU")
     ap.add_argument("--workload", default="uniform", choices=["uniform", "dedup", "zeros"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the cpu_baseline leg (0: the job's CPU share)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="N=1: chunking jobs kept in flight (one library context each), so "
                          "the host's wait for job k overlaps the GPU work of job k+1")
@@ -50,6 +51,11 @@ def parse():
                     help="N>1: compare the concatenated per-rank cut lists with one "
                          "dsx_cut_device over the whole blob on rank 0 (small sizes)")
     return ap.parse_args()
+
+
+DATA_LABEL = {"uniform": "uniform, splitmix64 seed 1 (dsx_gen_uniform)",
+              "dedup": "dedup, seed 2, 30 % of 1 MiB blocks copy earlier ones (dsx_gen_dedup)",
+              "zeros": "zeros"}
 
 
 def make_blob(ctx, t, offset, n, workload):
@@ -79,36 +85,82 @@ def load_traffic(workload, nbytes):
     return None
 
 
-def cpu_baseline(host_blob, threads):
-    """make.go-style split-and-align (C restatement, oracle/) on host cores."""
+def cpu_share():
+    """Host threads this job may use: the GPU box exports OMP_NUM_THREADS (16,
+    its CPU share for one GPU); nproc / os.cpu_count() there report the whole
+    machine, which a one-GPU job must not take."""
+    try:
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        return max(1, min(os.cpu_count() or 1, 16))
+
+
+def _cpu_leg(sample, threads, budget_s):
+    """Repeat oracle.chunk_parallel over the sample until ~budget_s core-seconds."""
     from oracle import oracle as o
-    sample = host_blob
-    n = sample.size
-    # single thread on a 128 MiB prefix
-    pre = sample[:128 << 20]
-    t0 = time.perf_counter()
-    o.chunk_stream(pre, MIN, AVG, MAX)
-    st = time.perf_counter() - t0
-    # threads: repeat the full sample until ~10 s of CPU work
-    reps, t_total, done = 0, 0.0, 0
+    o.chunk_parallel(sample[:64 << 20], MIN, AVG, MAX, threads)  # threads + pages warm
+    reps, t_total = 0, 0.0
     while True:
         t0 = time.perf_counter()
         o.chunk_parallel(sample, MIN, AVG, MAX, threads)
         t_total += time.perf_counter() - t0
         reps += 1
-        done += n
-        if t_total * threads >= 10.0 or reps >= 20:
+        if t_total * threads >= budget_s or reps >= 20:
             break
+    return reps, reps * sample.size / t_total / GiB
+
+
+def _ids_rate(sample, threads):
+    """SHA-512/256 chunk IDs on the host (hashlib releases the GIL), reported
+    separately as BASELINE.md's plan asks."""
+    import concurrent.futures as cf
+    import hashlib
+    from oracle import oracle as o
+    ends = o.chunk_parallel(sample, MIN, AVG, MAX, threads).tolist()
+    starts = [0] + ends[:-1]
+    mv = memoryview(sample)
+
+    def h(i):
+        z = hashlib.new("sha512_256")
+        z.update(mv[starts[i]:ends[i]])
+        return z.digest()
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as pool:
+        for _ in pool.map(h, range(len(ends)), chunksize=64):
+            pass
+    return sample.size / (time.perf_counter() - t0) / GiB
+
+
+def cpu_baseline(host_blob, threads=None):
+    """make.go-style split-and-align (C restatement, oracle/) on the host:
+    at the job's CPU share and at n = 10 (desync make's default -n), plus one
+    thread and the SHA-512/256 ID rate."""
+    from oracle import oracle as o
+    threads = threads or cpu_share()
+    sample = host_blob
+    n = sample.size
+    pre = sample[:128 << 20]
+    t0 = time.perf_counter()
+    o.chunk_stream(pre, MIN, AVG, MAX)
+    single = pre.size / (time.perf_counter() - t0) / GiB
+    reps, rate = _cpu_leg(sample, threads, 10.0)
+    reps10, rate10 = _cpu_leg(sample, 10, 8.0)
+    ids = _ids_rate(sample[:256 << 20], threads)
     return {
-        "value": round(done / t_total / GiB, 3),
+        "value": round(rate, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
         "sample": (f"{reps}x the same {n / GiB:.2f} GiB blob, C restatement of desync's "
                    f"Chunker.Next loop with make.go split-and-align over {threads} threads "
-                   f"(oracle/dsx_oracle.c, in memory, no chunk IDs); single-thread "
-                   f"{pre.size / st / GiB:.3f} GiB/s on 128 MiB"),
-        "single_thread_gibs": round(pre.size / st / GiB, 3),
+                   f"(the job's CPU share; oracle/dsx_oracle.c, in memory, no chunk IDs); "
+                   f"n=10 (desync make default): {rate10:.3f} GiB/s over {reps10}x; "
+                   f"single thread {single:.3f} GiB/s on 128 MiB; SHA-512/256 IDs "
+                   f"{ids:.3f} GiB/s over {threads} threads on 256 MiB"),
+        "n10_gibs": round(rate10, 3),
+        "single_thread_gibs": round(single, 3),
+        "ids_sha512_256_gibs": round(ids, 3),
     }
 
 
@@ -264,7 +316,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic ({args.workload}, splitmix64 seed 1, generated on device)",
+            "data": f"synthetic ({DATA_LABEL[args.workload]}, generated on device)",
             "config": {
                 "workload": (f"{args.gib:g} GiB {args.workload} blob per GPU, desync make "
                              f"min/avg/max 16/64/256 KiB, device-resident blob -> cut list in HBM"),
@@ -291,7 +343,7 @@ def main():
             }
         if world == 1 and not args.no_cpu:
             host = blob[halo:].cpu().numpy()
-            res["cpu_baseline"] = cpu_baseline(host, args.cpu_threads)
+            res["cpu_baseline"] = cpu_baseline(host, args.cpu_threads or None)
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
