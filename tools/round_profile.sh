@@ -22,3 +22,9 @@ for w in dedup zeros; do
   timeout -k 10 300 python bench.py --workload $w --gib 4 --no-cpu > $OUT/bench_$w.json 2> $OUT/bench_$w.err || { tail $OUT/bench_$w.err; exit 1; }
   cat $OUT/bench_$w.json
 done
+timeout -k 10 300 python tools/digest_rate.py 1 4 16 > $OUT/digest_rate.json 2> $OUT/digest_rate.err || { tail $OUT/digest_rate.err; exit 1; }
+cat $OUT/digest_rate.json
+timeout -k 10 300 python tools/make_rate.py > $OUT/make_rate.json 2> $OUT/make_rate.err || { tail $OUT/make_rate.err; exit 1; }
+cat $OUT/make_rate.json
+timeout -k 10 300 python tools/stream_rate.py > $OUT/stream_rate.json 2> $OUT/stream_rate.err || { tail $OUT/stream_rate.err; exit 1; }
+cat $OUT/stream_rate.json
