@@ -1,9 +1,11 @@
 """Chunk ID digests (digest.go:11-29, nullchunk.go:17-23).
 
 ``Digest`` is the package-global algorithm (SHA-512/256 by default, SHA-256
-alternative), as in the reference.  These run on the host (Go stdlib crypto
-in the reference; OpenSSL via hashlib here).  A GPU SHA-512/256 kernel is the
-next item of the hot path.
+alternative), as in the reference.  It selects the algorithm; the chunk IDs of
+the product paths are computed on the GPU with it (digest_kernel behind
+dsx_chunk_ids, dsx_index_fd / dsx_index_host and dsx_stream_ids: IndexFromFile,
+VerifyIndex, ChunkStream).  ``Digest.Sum`` here is the host form (hashlib) for
+a single buffer a caller holds, as the reference's Digest.Sum is.
 """
 from __future__ import annotations
 
