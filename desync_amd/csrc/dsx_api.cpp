@@ -174,6 +174,8 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SCAN_VARIANT")) c->variant = atoi(v);
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
 #endif
+  if (const char* v = getenv("DSX_DIGEST_PC")) c->digest_pc = atoi(v);
+  if (const char* v = getenv("DSX_DIGEST_PC_CHUNKS")) c->digest_pc_chunks = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
@@ -922,6 +924,25 @@ extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream,
                   uint32_t* queue) {
   if (!stream) stream = c->stream;
+  if (!queue) {
+    HIPCHK(c, c->dg_queue.ensure(1));
+    queue = c->dg_queue.p;
+  }
+  // split producer/consumer kernel: one workgroup (producer + consumer wave)
+  // per CU, up to digest_pc_chunks chunks per lane of the grid
+  const uint64_t pc_lanes = (uint64_t)c->ncu * 64u;
+  if (c->digest_pc > 0 || (c->digest_pc < 0 && max_n <= pc_lanes * (uint64_t)c->digest_pc_chunks)) {
+    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((max_n + 63) / 64, c->ncu));
+    HIPCHK(c, hipMemsetAsync(queue, 0, 4, stream));
+    da.queue = queue;
+    da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * 64u);
+    if (algo == DSX_DIGEST_SHA512_256)
+      hipLaunchKernelGGL(digest_pc_kernel<Sha512>, dim3((uint32_t)blocks), dim3(128), 0, stream, da);
+    else
+      hipLaunchKernelGGL(digest_pc_kernel<Sha256>, dim3((uint32_t)blocks), dim3(128), 0, stream, da);
+    HIPCHK(c, hipGetLastError());
+    return DSX_OK;
+  }
   // Lanes: exactly the workgroups that are resident at once (occupancy is set
   // by VGPRs: 2 per CU for SHA-512, 3 for SHA-256), every lane pulling chunks
   // from the queue.  A larger grid would hand its non-resident workgroups a
@@ -937,10 +958,6 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
   const uint64_t blocks = std::max<uint64_t>(
       1, std::min<uint64_t>((max_n + kDigestThreads - 1) / kDigestThreads,
                             (uint64_t)per_cu * (uint64_t)c->ncu));
-  if (!queue) {
-    HIPCHK(c, c->dg_queue.ensure(1));
-    queue = c->dg_queue.p;
-  }
   HIPCHK(c, hipMemsetAsync(queue, 0, 4, stream));
   da.queue = queue;
   da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * kDigestThreads);

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "dsx_digest.h"
 #include "dsx_stitch.h"
@@ -90,19 +91,67 @@ __device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) 
 __device__ __forceinline__ uint32_t maj32(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
+// A 64-bit value from its halves, opaque to the optimizer: left visible, the
+// (hi << 32) | lo feeding a 64-bit add is split into two adds (zero-extended
+// lo, then hi << 32) with a v_mov for each zero half -- 3 extra instructions
+// per SHA-512 round.  The empty asm makes it one register pair.
+__device__ __forceinline__ uint64_t pair64(uint32_t lo, uint32_t hi) {
+  uint64_t v = ((uint64_t)hi << 32) | lo;
+  asm("" : "+v"(v));  // (not volatile: no scheduling barrier)
+  return v;
+}
 __device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
-  return ((uint64_t)xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
-         xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+  return pair64(xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c),
+                xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)));
 }
 __device__ __forceinline__ uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
-  return ((uint64_t)maj32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
-         maj32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+  return pair64(maj32((uint32_t)a, (uint32_t)b, (uint32_t)c),
+                maj32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)));
+}
+// SHA's Ch(e, f, g) = (e & f) ^ (~e & g): one v_bfi_b32 per dword
+__device__ __forceinline__ uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) {
+  return pair64(((uint32_t)e & (uint32_t)f) ^ (~(uint32_t)e & (uint32_t)g),
+                ((uint32_t)(e >> 32) & (uint32_t)(f >> 32)) ^ (~(uint32_t)(e >> 32) & (uint32_t)(g >> 32)));
 }
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
   return __builtin_amdgcn_perm(x, x, 0x00010203u);
+}
+
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Hand-issued LDS reads for digest_pc_kernel's consumer (see compress_kw).
+typedef __attribute__((address_space(3))) const void lds_cvoid_t;
+template <int OFF>
+__device__ __forceinline__ void lds_read64(uint64_t& v, uint32_t addr) {
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void lds_read32(uint32_t& v, uint32_t addr) {
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+}
+// wait until at most n LDS reads are outstanding (n: compile-time after unrolling)
+template <class T>
+__device__ __forceinline__ void lds_wait_for(T& v, int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v)); break;
+    case 1: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(v)); break;
+    case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(v)); break;
+    case 3: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(v)); break;
+    case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(v)); break;
+    case 5: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(v)); break;
+    case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(v)); break;
+    default: asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(v)); break;
+  }
 }
 
 // A block as 32 big-endian-assembled dwords (SHA-512: 16 words = 32 dwords,
@@ -161,6 +210,58 @@ struct Sha512 {
       o[2 * i + 1] = bswap32((uint32_t)H[i]);
     }
   }
+
+  // ---- split form (digest_pc_kernel): the message schedule on a producer
+  // wave, the 80 rounds on a consumer wave, K[t] + W[t] handed over in LDS
+  using Word = uint64_t;
+  static constexpr int ROUNDS = 80;
+  // kw[t * 64] = K[t] + W[t] for the block d (one lane's column of the LDS buffer)
+  __device__ static void schedule(const uint32_t (&d)[32], Word* kw) {
+    uint64_t W[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) W[i] = ((uint64_t)d[2 * i] << 32) | d[2 * i + 1];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) kw[j * 64] = W[j] + kK512[j];
+#pragma unroll 1
+    for (int t0 = 16; t0 < 80; t0 += 16) {
+      uint64_t K[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) K[j] = kK512[t0 + j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
+        const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+        const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
+        W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
+        kw[(t0 + j) * 64] = W[j] + K[j];
+      }
+    }
+  }
+  // the 80 rounds on K[t] + W[t] read from LDS at kw + t * 64 words.  The
+  // reads are issued by hand 8 rounds ahead (the compiler placed each one a
+  // few instructions before its use, exposing the LDS latency every round);
+  // the compiler does not count them, so each use waits explicitly.
+  __device__ void compress_kw(const Word* kw) {
+    const uint32_t base = (uint32_t)(uintptr_t)(const lds_cvoid_t*)kw;
+    uint64_t L[9];
+    sfor<8>([&](auto tc) __attribute__((always_inline)) {
+      lds_read64<decltype(tc)::value * 512>(L[decltype(tc)::value], base);
+    });
+    uint64_t a = H[0], b = H[1], c = H[2], dd = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+    sfor<80>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value;
+      lds_wait_for(L[t % 9], 79 - t < 7 ? 79 - t : 7);
+      const uint64_t kwt = L[t % 9];
+      if constexpr (t + 8 < 80) lds_read64<(t + 8) * 512>(L[(t + 8) % 9], base);
+      const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+      const uint64_t ch = ch64(e, f, g);
+      const uint64_t t1 = h + S1 + ch + kwt;
+      const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+      const uint64_t t2 = S0 + maj64(a, b, c);
+      h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
+    });
+    H[0] += a; H[1] += b; H[2] += c; H[3] += dd; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+  }
 };
 
 struct Sha256 {
@@ -208,6 +309,51 @@ struct Sha256 {
     uint32_t* o = reinterpret_cast<uint32_t*>(dst);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = bswap32(H[i]);
+  }
+
+  using Word = uint32_t;
+  static constexpr int ROUNDS = 64;
+  __device__ static void schedule(const uint32_t (&d)[32], Word* kw) {
+    uint32_t W[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) W[i] = d[i];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) kw[j * 64] = W[j] + kK256[j];
+#pragma unroll 1
+    for (int t0 = 16; t0 < 64; t0 += 16) {
+      uint32_t K[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) K[j] = kK256[t0 + j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
+        const uint32_t s0 = xor3_32(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3_32(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+        W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
+        kw[(t0 + j) * 64] = W[j] + K[j];
+      }
+    }
+  }
+  __device__ void compress_kw(const Word* kw) {
+    const uint32_t base = (uint32_t)(uintptr_t)(const lds_cvoid_t*)kw;
+    uint32_t L[9];
+    sfor<8>([&](auto tc) __attribute__((always_inline)) {
+      lds_read32<decltype(tc)::value * 256>(L[decltype(tc)::value], base);
+    });
+    uint32_t a = H[0], b = H[1], c = H[2], dd = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+    sfor<64>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value;
+      lds_wait_for(L[t % 9], 63 - t < 7 ? 63 - t : 7);
+      const uint32_t kwt = L[t % 9];
+      if constexpr (t + 8 < 64) lds_read32<(t + 8) * 256>(L[(t + 8) % 9], base);
+      const uint32_t S1 = xor3_32(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+      const uint32_t ch = (e & f) ^ (~e & g);
+      const uint32_t t1 = h + S1 + ch + kwt;
+      const uint32_t S0 = xor3_32(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+      const uint32_t t2 = S0 + maj32(a, b, c);
+      h = g; g = f; f = e; e = dd + t1; dd = c; c = b; b = a; a = t1 + t2;
+    });
+    H[0] += a; H[1] += b; H[2] += c; H[3] += dd; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
   }
 };
 
@@ -405,5 +551,143 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
 
 template __global__ void digest_kernel<Sha512>(DigestArgs);
 template __global__ void digest_kernel<Sha256>(DigestArgs);
+
+// ---------------------------------------------------------------------------
+// digest_pc_kernel -- the same IDs with each chunk's work split over two waves.
+//
+// A lone wave issues one VALU instruction every ~5 cycles (tools/ubench_hash),
+// and at small blobs the time is the longest chunk's serial chain of block
+// compressions (2048 blocks for a 256 KiB chunk).  A block is ~40 % message
+// schedule, which does not depend on the chaining state: here a producer wave
+// (wave 0) assembles each lane's next block and writes its 80 (64) round
+// inputs K[t] + W[t] to LDS while the consumer wave (wave 1) runs the rounds
+// of the previous block on them.  Lane l of both waves serves the same chunk
+// sequence; the producer owns the chunk state machine and the queue, and
+// hands each block over with a record {flags, chunk index}.  One barrier per
+// block; two LDS buffers.  The LDS size keeps one workgroup per CU, so the
+// consumer wave has its SIMD to itself.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPcLds = 84 * 1024;
+template <class H>
+__global__ __launch_bounds__(128, 1) void digest_pc_kernel(DigestArgs a) {
+  using Word = typename H::Word;
+  constexpr int BLK = H::BLK;
+  constexpr int R = H::ROUNDS;
+  constexpr uint32_t KWB = (uint32_t)R * 64u * sizeof(Word);  // one buffer
+  static_assert(2 * KWB + 1024 + 16 <= kPcLds, "LDS layout");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kPcLds];
+  Word* kwbuf = reinterpret_cast<Word*>(lds);                   // [2][R][64]
+  uint32_t* rflag = reinterpret_cast<uint32_t*>(lds + 2 * KWB);  // [2][64]
+  uint32_t* rci = rflag + 128;                                   // [2][64]
+  uint32_t* live = rci + 128;                                    // [2]
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool producer = threadIdx.x < 64u;
+  uint64_t n = a.n, first_start = a.first_start;
+  uint32_t nfirst = a.nfirst;
+  const uint64_t* ends = a.ends;
+  uint8_t* ids = a.ids;
+  if (a.range_lo) {
+    const uint64_t i0 = a.range_lo[0], i1 = a.range_hi[0];
+    n = i1 > i0 ? i1 - i0 : 0;
+    first_start = a.range_lo[1];
+    ends += i0;
+    ids += i0 * 32u;
+    const uint64_t lanes = (uint64_t)gridDim.x * 64u;
+    nfirst = (uint32_t)(n < lanes ? n : lanes);
+  }
+  // producer: chunk state (s, e, pos relative to blob[0])
+  uint64_t ci = (uint64_t)blockIdx.x * 64u + lane;
+  uint64_t s = 0, e = 0, pos = 0;
+  uint32_t phase = 0;
+  uint32_t raw[BLK / 4 + 4];
+  bool have_next = false, fresh = true;
+  auto start_chunk = [&]() {
+    while (ci < n) {
+      const uint64_t sa = ci == 0 ? first_start : ends[ci - 1], ea = ends[ci];
+      if (sa >= a.base_off && sa <= ea && ea - a.base_off <= a.len) {
+        s = sa - a.base_off;
+        e = ea - a.base_off;
+        pos = s;
+        phase = 0;
+        have_next = false;
+        fresh = true;
+        return;
+      }
+      ci = n;
+    }
+  };
+  if (producer) {
+    if (ci >= nfirst) ci = n;
+    start_chunk();
+  }
+  H st;  // consumer: chaining state of the lane's current chunk
+  for (uint32_t k = 0;; ++k) {
+    const uint32_t b = k & 1u;
+    if (producer) {
+      const bool lv = ci < n;
+      bool fin = false;
+      if (lv) {
+        uint32_t d[32];
+        const uint64_t r = e - pos;
+        if (phase == 0 && r >= (uint64_t)BLK) {
+          if (have_next) {
+            align_raw<BLK>(raw, pos, d);
+          } else if (fast_ok<BLK>(pos, a.len)) {
+            fetch_raw<BLK>(a.blob, pos, raw);
+            align_raw<BLK>(raw, pos, d);
+          } else {
+            load_block_bytes<BLK>(a.blob, pos, d);
+          }
+          pos += BLK;
+          have_next = e - pos >= (uint64_t)BLK && fast_ok<BLK>(pos, a.len);
+          if (have_next) fetch_raw<BLK>(a.blob, pos, raw);
+        } else {
+          const uint64_t bits = (e - s) * 8u;
+          if (phase == 0) {
+            const bool fits = r < (uint64_t)(BLK - H::LENB);
+            tail_block<BLK, H::LENB>(a.blob + pos, (uint32_t)r, true, fits, bits, d);
+            pos = e;
+            phase = fits ? 3 : 2;
+          } else {
+            tail_block<BLK, H::LENB>(a.blob + pos, 0u, false, true, bits, d);
+            phase = 3;
+          }
+        }
+        H::schedule(d, kwbuf + b * (uint32_t)R * 64u + lane);
+        fin = phase == 3;
+      }
+      rflag[b * 64u + lane] = lv ? (1u | (fresh ? 2u : 0u) | (fin ? 4u : 0u)) : 0u;
+      rci[b * 64u + lane] = (uint32_t)ci;
+      fresh = false;
+      const uint64_t lm = __ballot(lv);
+      if (lane == 0) live[b] = lm != 0 ? 1u : 0u;
+      // refill the lanes whose chunk ended with this block (one atomic per wave)
+      const uint64_t fm = __ballot(fin);
+      if (fm) {
+        const uint32_t nf = (uint32_t)__popcll(fm);
+        uint32_t base = 0;
+        if (lane == (uint32_t)(__ffsll((long long)fm) - 1)) base = atomicAdd(a.queue, nf);
+        base = __shfl(base, __ffsll((long long)fm) - 1, 64);
+        if (fin) {
+          const uint32_t rank = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+          ci = (uint64_t)nfirst + base + rank;
+          start_chunk();
+        }
+      }
+    } else if (k > 0) {
+      const uint32_t pb = b ^ 1u;
+      if (live[pb]) {
+        const uint32_t f = rflag[pb * 64u + lane];
+        if (f & 2u) st.init();
+        st.compress_kw(kwbuf + pb * (uint32_t)R * 64u + lane);
+        if (f & 4u) st.out(ids + (uint64_t)rci[pb * 64u + lane] * 32u);
+      }
+    }
+    __syncthreads();
+    if (!live[b]) break;
+  }
+}
+template __global__ void digest_pc_kernel<Sha512>(DigestArgs);
+template __global__ void digest_pc_kernel<Sha256>(DigestArgs);
 
 }  // namespace dsx

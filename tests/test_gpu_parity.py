@@ -496,6 +496,36 @@ def test_chunk_ids_match_hashlib(dctx, algo):
         assert got[i] == want, (i, s, e)
 
 
+@pytest.mark.parametrize("pc", ["0", "1"])
+@pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
+def test_chunk_ids_both_kernels(monkeypatch, pc, algo):
+    """Both digest kernels (DSX_DIGEST_PC=0: one wave per chunk set; 1: the
+    producer/consumer split) on the padding cases and on 120 K short chunks --
+    several per lane of either grid, so the queue refills lanes mid-run."""
+    import hashlib
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_DIGEST_PC", pc)
+    ctx = _lib.Context(0)
+    try:
+        rng = np.random.default_rng(11)
+        total = (40 << 20) + 7
+        arr = rng.integers(0, 256, size=total, dtype=np.uint8)
+        t = torch_dev(arr)
+        code = _lib.DSX_DIGEST_SHA512_256 if algo == "sha512-256" else _lib.DSX_DIGEST_SHA256
+        name = "sha512_256" if algo == "sha512-256" else "sha256"
+        buf = arr.tobytes()
+        short = np.cumsum(rng.integers(0, 600, size=120_000)).astype(np.uint64)
+        short = short[short <= total]
+        for ends in (_tricky_ends(total, rng), short):
+            got = desync_amd.chunk_ids(t.data_ptr(), total, ends, 0, ctx=ctx, algo=code)
+            starts = np.concatenate([np.zeros(1, np.uint64), ends[:-1]])
+            for i, (s0, e0) in enumerate(zip(starts.tolist(), ends.tolist())):
+                assert got[i] == hashlib.new(name, buf[s0:e0]).digest(), (i, s0, e0)
+    finally:
+        ctx.close()
+
+
 def test_chunk_ids_default_chunking(dctx):
     """IDs of the real chunking of a 64 MiB seeded blob (config-2 shape)."""
     import hashlib
