@@ -103,7 +103,7 @@ struct dsx_ctx {
   int scan_cfg = 0;                   // DSX_SCAN_CFG: index into kCfg* (waves, rounds/batch, LDS buffers)
   bool scan_line = true;              // DSX_SCAN_LINE=0: 96-B-row scan_kernel instead of scanl_kernel
   int digest_pc = -1;                 // DSX_DIGEST_PC: 1 producer/consumer digest kernel, 0 the one-wave kernel, -1 by size
-  int digest_pc_chunks = 8;           // DSX_DIGEST_PC_CHUNKS: auto uses it up to this many chunks per grid lane
+  int digest_pc_chunks = 2;           // DSX_DIGEST_PC_CHUNKS: auto uses it up to this many chunks per grid lane
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
   uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
