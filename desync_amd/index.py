@@ -11,12 +11,17 @@ import io
 import struct
 from dataclasses import dataclass, field
 
+import numpy as np
+
 CaFormatEntry = 0x1396FABCEA5BBB51
 CaFormatIndex = 0x96824D9C7B129FF9
 CaFormatTable = 0xE75B9E112F17417D
 CaFormatTableTailMarker = 0x4B4F050E5549ECD1
 CaFormatSHA512256 = 0x2000000000000000
 CaFormatExcludeNoDump = 0x8000000000000000
+
+
+_ITEM = np.dtype([("off", "<u8"), ("id", "S32")])
 
 
 class InvalidFormat(ValueError):
@@ -31,7 +36,7 @@ class FormatIndex:
     ChunkSizeMax: int = 0
 
 
-@dataclass
+@dataclass(slots=True)
 class IndexChunk:
     ID: bytes
     Start: int
@@ -54,12 +59,14 @@ class Index:
         out = bytearray(struct.pack("<6Q", 48, CaFormatIndex, fi.FeatureFlags, fi.ChunkSizeMin,
                                     fi.ChunkSizeAvg, fi.ChunkSizeMax))
         out += struct.pack("<2Q", 0xFFFFFFFFFFFFFFFF, CaFormatTable)
-        n = 16
-        offset = 0
-        for c in self.Chunks:
-            offset += c.Size
-            out += struct.pack("<Q", offset) + bytes(c.ID)
-            n += 40
+        # table items {end offset, ID} (format.go:596-605), packed in one go
+        nc = len(self.Chunks)
+        items = np.empty(nc, dtype=_ITEM)
+        if nc:
+            items["off"] = np.cumsum(np.fromiter((c.Size for c in self.Chunks), np.uint64, nc))
+            items["id"] = np.frombuffer(b"".join(bytes(c.ID) for c in self.Chunks), "S32")
+        out += items.tobytes()
+        n = 16 + 40 * nc
         # tail record: zero fill x2, index offset, table size, marker (format.go:607-614)
         out += struct.pack("<5Q", 0, 0, 48, n + 40, CaFormatTableTailMarker)
         return bytes(out)
