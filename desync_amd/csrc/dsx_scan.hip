@@ -534,11 +534,13 @@ DSX_SCAN_INST(2, 2, 8, 8, true)
 #if DSX_DIAG
 DSX_SCAN_INST_DIAG(2, 2, 8, 8, false)
 DSX_SCAN_INST_DIAG(2, 2, 8, 8, true)
-DSX_SCAN_INST(1, 2, 12, 4, false)
-DSX_SCAN_INST(1, 2, 16, 4, false)
-DSX_SCAN_INST(2, 1, 12, 8, false)
-DSX_SCAN_INST(2, 1, 8, 8, false)
-DSX_SCAN_INST(2, 1, 16, 4, false)
+#define DSX_SCAN_INST_ALL(BR, NBUF, W, SUB, PF) \
+  DSX_SCAN_INST(BR, NBUF, W, SUB, PF) DSX_SCAN_INST_DIAG(BR, NBUF, W, SUB, PF)
+DSX_SCAN_INST_ALL(1, 2, 12, 4, false)
+DSX_SCAN_INST_ALL(1, 2, 16, 4, false)
+DSX_SCAN_INST_ALL(2, 1, 12, 8, false)
+DSX_SCAN_INST_ALL(2, 1, 8, 8, false)
+DSX_SCAN_INST_ALL(2, 1, 16, 4, false)
 #endif
 
 // ---------------------------------------------------------------------------
