@@ -97,6 +97,42 @@ def test_index_host_two_gib_windows():
     assert [bytes(x) for x in ids] == want
 
 
+def test_urandom_file(tmp_path):
+    """SURVEY.md 8(d) config 2's extra run: 1 GiB of real /dev/urandom bytes
+    saved to a file, so the CPU oracle sees exactly the bytes the GPU chunked
+    (dsx_index_fd: cuts and IDs)."""
+    import concurrent.futures as cf
+
+    import desync_amd
+    n = 1 << 30
+    f = tmp_path / "urandom.bin"
+    with open("/dev/urandom", "rb") as src, open(f, "wb") as dst:
+        left = n
+        while left:
+            b = src.read(min(left, 64 << 20))
+            dst.write(b)
+            left -= len(b)
+    data = np.fromfile(str(f), dtype=np.uint8)
+    fd = os.open(str(f), os.O_RDONLY)
+    try:
+        ends, ids = desync_amd.index_fd(fd, MIN, AVG, MAX)
+    finally:
+        os.close(fd)
+    ref = o.chunk_parallel(data, MIN, AVG, MAX, o.default_threads())
+    assert np.array_equal(ends, ref)
+    starts = np.concatenate([[0], ref[:-1]]).astype(np.uint64)
+    mv = memoryview(data)
+
+    def h(i):
+        z = hashlib.new("sha512_256")
+        z.update(mv[int(starts[i]):int(ref[i])])
+        return z.digest()
+
+    with cf.ThreadPoolExecutor(o.default_threads()) as pool:
+        want = list(pool.map(h, range(ref.size), chunksize=256))
+    assert [bytes(x) for x in ids] == want
+
+
 def test_empty_file_and_sha256_flags(tmp_path, golden):
     """The empty file gives the 104-byte caibx (header + table marker + tail);
     under --digest sha256 the index flags lack CaFormatSHA512256
