@@ -194,9 +194,6 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   }
   CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-  CREATE_STEP(hipEventCreate(&c->ev_t0));
-  CREATE_STEP(hipEventCreate(&c->ev_t1));
-  CREATE_STEP(hipEventCreate(&c->ev_t2));
   for (int i = 0; i < 2; ++i) {
     CREATE_STEP(hipEventCreateWithFlags(&c->copy_done[i], hipEventDisableTiming));
     CREATE_STEP(hipEventCreateWithFlags(&c->comp_done[i], hipEventDisableTiming));
@@ -239,7 +236,7 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   if (c->h_ring) (void)hipHostFree(c->h_ring);
   for (uint32_t i = 0; i < kQueueDepth; ++i)
     if (c->q_ev[i]) (void)hipEventDestroy(c->q_ev[i]);
-  hipEvent_t evs[] = {c->ev_t0, c->ev_t1, c->ev_t2, c->copy_done[0], c->copy_done[1],
+  hipEvent_t evs[] = {c->copy_done[0], c->copy_done[1],
                       c->comp_done[0], c->comp_done[1]};
   for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
@@ -450,7 +447,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     HIPCHK(c, hipEventCreate(&e));
     c->pev.push_back(e);
   }
-  HIPCHK(c, hipEventRecord(c->pev[3 * pi], c->stream));
+  if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi], c->stream));
   {
     const uint64_t need_wg = std::max<uint64_t>(1, (nregions + W - 1) / W);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)c->ncu);
@@ -520,7 +517,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
 #undef DSX_TRACE_VARIANTS
     HIPCHK(c, hipGetLastError());
   }
-  HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));
+  if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));
   PieceCands pc{};
   pc.P = c->last_grid_P;  // region r covers (P' + r*RB, P' + (r+1)*RB]
   pc.RB = region_bytes;
@@ -536,7 +533,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   }
   int rc = launch_stitch(c, cc, pc, P, len, is_last, seq, line && c->scan_trace);
   if (rc) return rc;
-  HIPCHK(c, hipEventRecord(c->pev[3 * pi + 2], c->stream));
+  if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi + 2], c->stream));
   c->stats.pieces++;
   return DSX_OK;
 }
@@ -687,18 +684,8 @@ extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
   }
   c->stats.chunks = s.total;
   c->stats.repaired_segments = s.repaired;
-  if (c->pend.empty()) {  // timing events belong to the last enqueued call
-    float scan = 0, stitch = 0;
-    for (uint32_t i = 0; i < c->npiece_call; ++i) {
-      float a = 0, b = 0;
-      (void)hipEventElapsedTime(&a, c->pev[3 * i], c->pev[3 * i + 1]);
-      (void)hipEventElapsedTime(&b, c->pev[3 * i + 1], c->pev[3 * i + 2]);
-      scan += a;
-      stitch += b;
-    }
-    c->stats.scan_ms = scan;
-    c->stats.stitch_ms = stitch;
-  }
+  c->stats.scan_ms = 0;  // queued calls are not timed (no events between their kernels)
+  c->stats.stitch_ms = 0;
   *n_out = s.total;
   if ((s.err & kErrCapacity) || s.total > q.cap) return DSX_E_CAPACITY;
   return DSX_OK;
@@ -729,11 +716,13 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
     q.slot = c->q_next++ % kQueueDepth;
     q.done = c->q_ev[q.slot];
     c->h_cur = &c->h_ring[q.slot];
-    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
+    // queued calls record no timing events: an event record between two
+    // kernels of a stream costs ~6 us of GPU time (rocprofv3 kernel trace)
+    c->timing = false;
     rc = run_device(c, (const uint8_t*)d_blob, len, cc);
+    c->timing = true;
     c->h_cur = c->h_state;
     if (rc) return rc;
-    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
     HIPCHK(c, hipEventRecord(q.done, c->stream));
     q.seq = c->piece_seq;
     c->pend.push_back(q);
@@ -749,10 +738,8 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
       cc.d_out = c->out.p;
       cc.out_cap = need;
     }
-    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
     rc = run_device(c, (const uint8_t*)d_blob, len, cc);
     if (rc) return rc;
-    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
     bool dense = false;
     rc = finish_call(c, n_out, dev_out ? cap : need, &dense);
     if (dense) {
@@ -800,7 +787,6 @@ static int run_host_pipeline(dsx_ctx* c, const dsx_params_t* p, uint64_t len,
     CallCfg cc{p, len, 0, kRound, c->out.p, need, dense};
     rc = reset_state(c, 0);
     if (rc) return rc;
-    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
     uint64_t i = 0;
     for (uint64_t off = 0; off < len; off += chunk, ++i) {
       if (c->cancel.load()) return DSX_E_INTERRUPTED;
@@ -821,7 +807,6 @@ static int run_host_pipeline(dsx_ctx* c, const dsx_params_t* p, uint64_t len,
       if (rc) return rc;
       HIPCHK(c, hipEventRecord(c->comp_done[b], c->stream));
     }
-    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
     bool dn = false;
     rc = finish_call(c, n_out, need, &dn);
     if (dn) {
@@ -1082,7 +1067,6 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
     CallCfg cc{p, sh.total, entry, kRound, c->out.p, need, dense};
     cc.halo0 = sh.start > 0 ? sh.halo : 0;
     int rc = DSX_OK;
-    HIPCHK(c, hipEventRecord(c->ev_t0, c->stream));
     if (stitch_only) {
       HIPCHK(c, c->zero_word.ensure(1));
       HIPCHK(c, hipMemsetAsync(c->zero_word.p, 0, 4, c->stream));
@@ -1132,7 +1116,6 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
                        (const uint64_t*)c->out.p, (const DevState*)c->state.p, sh.start, sh.len,
                        sh.total, wend0, entry, (is_last ? (uint32_t)DSX_SEAM_LAST : 0u) | rec_flags);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev_t1, c->stream));
     HostState st;
     rc = read_state(c, &st);
     if (rc) return rc;

@@ -91,7 +91,7 @@ struct dsx_ctx {
   int device = 0;
   int ncu = 256;
   hipStream_t stream = nullptr, copy_stream = nullptr;
-  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_t2 = nullptr;
+  bool timing = true;  // record the per-piece scan/stitch events (stats.scan_ms/stitch_ms)
   hipEvent_t copy_done[2] = {nullptr, nullptr}, comp_done[2] = {nullptr, nullptr};
   std::atomic<int> cancel{0};
   std::string err;

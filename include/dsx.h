@@ -311,7 +311,7 @@ typedef struct dsx_stats {
     uint64_t pieces;            /* scan pieces processed */
     uint64_t repaired_segments; /* segments that needed the sequential repair */
     uint64_t dense_fallbacks;   /* pieces processed on the dense-candidate path */
-    float scan_ms, stitch_ms;   /* device time of the last call (HIP events) */
+    float scan_ms, stitch_ms;   /* device time of the last synchronous call (HIP events; 0 after dsx_result) */
 } dsx_stats_t;
 int dsx_get_stats(dsx_ctx_t *ctx, dsx_stats_t *out);
 
