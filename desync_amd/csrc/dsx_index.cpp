@@ -231,8 +231,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           e = hipStreamWaitEvent(c->stream, c->idx_copy_ev[k % K], 0);
           if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: wait"));
           const uint64_t halo = w == 0 ? scanned : pre + (scanned - ws);
+          c->timing = false;  // (no event records between the pipeline's kernels)
           rc = enqueue_piece(c, cc, buf + pre + (scanned - ws), halo, scanned, end - scanned,
                              end == len);
+          c->timing = true;
           if (rc) return drain(c, pf, rc);
           scanned = end;
         }

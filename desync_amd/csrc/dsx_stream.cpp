@@ -142,6 +142,7 @@ int st_issue(dsx_ctx* c, uint64_t len, bool last) {
   }
   CallCfg cc{&s.p, P + len, s.origin, s.origin + kRound, s.dout[slot].p, bound, s.dense};
   c->h_cur = &s.hstate[slot];
+  c->timing = false;  // (no event records between the batches' kernels)
   int rc = DSX_OK;
   if (!s.dense) {
     rc = enqueue_piece(c, cc, s.dbuf[slot].p + halo, halo, P, len, last);
@@ -152,6 +153,7 @@ int st_issue(dsx_ctx* c, uint64_t len, bool last) {
     }
   }
   c->h_cur = c->h_state;
+  c->timing = true;
   if (rc) return rc;
   hipStream_t out_stream = c->stream;
   if (ids) {
