@@ -13,7 +13,7 @@ with HasChunk(id) and StoreChunk(chunk)).
 """
 from __future__ import annotations
 
-import concurrent.futures as cf
+import queue
 import threading
 
 from .index import CaFormatExcludeNoDump, CaFormatSHA512256, FormatIndex, Index, IndexChunk
@@ -85,27 +85,47 @@ def ChunkStream(ctx, c, ws, n):
     c.EnableIDs()
     storage = ChunkStorage(ws)
     chunks = []
-    pending = set()
-    with cf.ThreadPoolExecutor(max_workers=max(1, int(n))) as pool:
-        try:
-            while True:
-                if ctx is not None and getattr(ctx, "done", lambda: False)():
-                    break
-                start, b = c.Next()
-                if not b:
-                    break
-                cid = c.ChunkID()
-                if cid is None:
-                    raise RuntimeError("chunker produced a chunk without a GPU chunk ID")
-                data = bytes(b)  # slices.Clone (index.go:196-200)
-                chunks.append(IndexChunk(ID=cid, Start=start, Size=len(data)))
-                pending.add(pool.submit(storage.StoreChunk, Chunk(cid, data)))
-                if len(pending) >= 4 * max(1, int(n)):  # bounded in-flight work, like the channel
-                    done, pending = cf.wait(pending, return_when=cf.FIRST_COMPLETED)
-                    for f in done:
-                        f.result()
-        finally:
-            for f in cf.as_completed(pending):
-                f.result()
+    nw = max(1, int(n))
+    # the reference's channel to n store goroutines (index.go:150-182): a
+    # bounded queue read by n threads; the first store error stops the
+    # producer, the workers drain what is queued without storing it
+    work = queue.Queue(maxsize=4 * nw)
+    errors = []
+
+    def worker():
+        while True:
+            ch = work.get()
+            if ch is None:
+                return
+            if errors:
+                continue
+            try:
+                storage.StoreChunk(ch)
+            except BaseException as e:  # noqa: BLE001 -- re-raised by the producer
+                errors.append(e)
+
+    threads = [threading.Thread(target=worker, daemon=True) for _ in range(nw)]
+    for t in threads:
+        t.start()
+    try:
+        while not errors:
+            if ctx is not None and getattr(ctx, "done", lambda: False)():
+                break
+            start, b = c.Next()
+            if not b:
+                break
+            cid = c.ChunkID()
+            if cid is None:
+                raise RuntimeError("chunker produced a chunk without a GPU chunk ID")
+            data = bytes(b)  # slices.Clone (index.go:196-200)
+            chunks.append(IndexChunk(cid, start, len(data)))
+            work.put(Chunk(cid, data))
+    finally:
+        for _ in threads:
+            work.put(None)
+        for t in threads:
+            t.join()
+    if errors:
+        raise errors[0]
     return Index(FormatIndex(CaFormatExcludeNoDump | CaFormatSHA512256, c.Min(), c.Avg(), c.Max()),
                  chunks)
