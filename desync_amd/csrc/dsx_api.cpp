@@ -194,10 +194,6 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   }
   CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-  for (int i = 0; i < 2; ++i) {
-    CREATE_STEP(hipEventCreateWithFlags(&c->copy_done[i], hipEventDisableTiming));
-    CREATE_STEP(hipEventCreateWithFlags(&c->comp_done[i], hipEventDisableTiming));
-  }
   CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
   CREATE_STEP(hipHostMalloc((void**)&c->h_ring, kQueueDepth * sizeof(HostState)));
   memset(c->h_ring, 0, kQueueDepth * sizeof(HostState));
@@ -228,17 +224,12 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   c->zero_word.release();
   c->d_seam.release(); c->d_all.release(); c->d_ext.release(); c->d_info.release(); c->d_emit.release();
   if (c->h_res) (void)hipHostFree(c->h_res);
-  c->dbuf[0].release(); c->dbuf[1].release();
   index_release(c);
   stream_release(c);
-  for (auto& p : c->pinned) if (p) (void)hipHostFree(p);
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
   for (uint32_t i = 0; i < kQueueDepth; ++i)
     if (c->q_ev[i]) (void)hipEventDestroy(c->q_ev[i]);
-  hipEvent_t evs[] = {c->copy_done[0], c->copy_done[1],
-                      c->comp_done[0], c->comp_done[1]};
-  for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -755,117 +746,6 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
   }
   c->err = "dense-candidate path overflowed";
   return DSX_E_INTERNAL;
-}
-
-// Host-resident pipeline: chunks of kHostChunk bytes are staged in pinned
-// memory and copied on copy_stream while the previous chunk is processed.
-static int run_host_pipeline(dsx_ctx* c, const dsx_params_t* p, uint64_t len,
-                             int (*fill)(void* ud, uint8_t* dst, uint64_t off, uint64_t n),
-                             void* ud, uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
-  HIPCHK(c, hipSetDevice(c->device));
-  c->cancel.store(0);
-  int rc = ensure_attr_walk(c);
-  if (rc) return rc;
-  *n_out = 0;
-  if (len == 0) return DSX_OK;
-  const uint64_t need = len / p->min + 2;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    const bool dense = attempt == 1;
-    const uint64_t chunk = dense ? kDensePiece : std::min<uint64_t>(kHostChunk, len);
-    const uint64_t buf_sz = chunk + 64;
-    if (c->pinned_sz < buf_sz) {
-      for (auto& b : c->pinned) {
-        if (b) (void)hipHostFree(b);
-        b = nullptr;
-        HIPCHK(c, hipHostMalloc((void**)&b, buf_sz));
-      }
-      c->pinned_sz = buf_sz;
-    }
-    HIPCHK(c, grow(c, c->dbuf[0], buf_sz));
-    HIPCHK(c, grow(c, c->dbuf[1], buf_sz));
-    HIPCHK(c, grow(c, c->out, need));
-    CallCfg cc{p, len, 0, kRound, c->out.p, need, dense};
-    rc = reset_state(c, 0);
-    if (rc) return rc;
-    uint64_t i = 0;
-    for (uint64_t off = 0; off < len; off += chunk, ++i) {
-      if (c->cancel.load()) return DSX_E_INTERRUPTED;
-      const int b = (int)(i & 1);
-      const uint64_t n = std::min(chunk, len - off);
-      const uint64_t h = std::min<uint64_t>(64, off);
-      // the pinned buffer b was last used by the copy two chunks ago
-      if (i >= 2) HIPCHK(c, hipEventSynchronize(c->copy_done[b]));
-      rc = fill(ud, c->pinned[b], off - h, n + h);
-      if (rc) return rc;
-      // device buffer b was last read by the compute two chunks ago
-      if (i >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->comp_done[b], 0));
-      HIPCHK(c, hipMemcpyAsync(c->dbuf[b].p, c->pinned[b], n + h, hipMemcpyHostToDevice,
-                               c->copy_stream));
-      HIPCHK(c, hipEventRecord(c->copy_done[b], c->copy_stream));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->copy_done[b], 0));
-      rc = enqueue_piece(c, cc, c->dbuf[b].p + h, h, off, n, off + n == len);
-      if (rc) return rc;
-      HIPCHK(c, hipEventRecord(c->comp_done[b], c->stream));
-    }
-    bool dn = false;
-    rc = finish_call(c, n_out, need, &dn);
-    if (dn) {
-      c->stats.dense_fallbacks++;
-      continue;
-    }
-    if (rc) return rc;
-    if (*n_out > cap) return DSX_E_CAPACITY;
-    if (*n_out)
-      HIPCHK(c, hipMemcpy(out_ends, c->out.p, *n_out * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    return DSX_OK;
-  }
-  c->err = "dense-candidate path overflowed";
-  return DSX_E_INTERNAL;
-}
-
-struct MemSrc {
-  const uint8_t* p;
-};
-static int fill_mem(void* ud, uint8_t* dst, uint64_t off, uint64_t n) {
-  memcpy(dst, ((MemSrc*)ud)->p + off, n);
-  return DSX_OK;
-}
-struct FdSrc {
-  int fd;
-  uint64_t base;
-};
-static int fill_fd(void* ud, uint8_t* dst, uint64_t off, uint64_t n) {
-  FdSrc* s = (FdSrc*)ud;
-  uint64_t got = 0;
-  while (got < n) {
-    const ssize_t r = pread(s->fd, dst + got, n - got, (off_t)(s->base + off + got));
-    if (r < 0) {
-      if (errno == EINTR) continue;
-      return DSX_E_IO;
-    }
-    if (r == 0) return DSX_E_IO;  // file shrank underneath us
-    got += (uint64_t)r;
-  }
-  return DSX_OK;
-}
-
-extern "C" int dsx_cut_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, const dsx_params_t* p,
-                            uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
-  if (!c || !p || !n_out || (len && !h_blob) || (cap && !out_ends)) return DSX_E_INVAL;
-  MemSrc s{(const uint8_t*)h_blob};
-  return run_host_pipeline(c, p, len, fill_mem, &s, out_ends, cap, n_out);
-}
-
-extern "C" int dsx_cut_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, const dsx_params_t* p,
-                          uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
-  if (!c || !p || !n_out || fd < 0 || (cap && !out_ends)) return DSX_E_INVAL;
-  if (len == UINT64_MAX) {
-    const off_t end = lseek(fd, 0, SEEK_END);
-    if (end < 0) return DSX_E_IO;
-    len = (uint64_t)end > off ? (uint64_t)end - off : 0;
-  }
-  FdSrc s{fd, off};
-  return run_host_pipeline(c, p, len, fill_fd, &s, out_ends, cap, n_out);
 }
 
 // --------------------------------------------------------------------------

@@ -48,7 +48,6 @@ using namespace dsx;
 namespace dsx_host {
 
 constexpr uint64_t kPieceMax = 8ull << 30;       // bytes per scan launch
-constexpr uint64_t kHostChunk = 256ull << 20;    // host-resident pipeline chunk
 constexpr uint64_t kStreamBatch = 16ull << 20;   // streaming: bytes per device batch
 constexpr uint32_t kQueueDepth = 8;              // DSX_NO_SYNC calls queued per context
 constexpr uint32_t kWalkLdsCap = 8192;           // candidates per walk workgroup (2 workgroups per CU)
@@ -92,7 +91,6 @@ struct dsx_ctx {
   int ncu = 256;
   hipStream_t stream = nullptr, copy_stream = nullptr;
   bool timing = true;  // record the per-piece scan/stitch events (stats.scan_ms/stitch_ms)
-  hipEvent_t copy_done[2] = {nullptr, nullptr}, comp_done[2] = {nullptr, nullptr};
   std::atomic<int> cancel{0};
   std::string err;
   int force_mode = -1;  // DSX_TEST_MODE env override
@@ -122,9 +120,6 @@ struct dsx_ctx {
   DevBuf<uint8_t> dg_ids;     // chunk IDs: staged digests
   DevBuf<uint32_t> dg_queue;  // chunk IDs: lane work queue
   DevBuf<DevState> state;
-  DevBuf<uint8_t> dbuf[2];
-  uint8_t* pinned[2] = {nullptr, nullptr};
-  size_t pinned_sz = 0;
   HostState* h_state = nullptr;  // pinned mirror published by fixup_kernel
   uint64_t piece_seq = 0;        // global piece counter (overflow parity, freshness)
   bool init_pending = false;     // next scan initialises DevState with init_carry

@@ -193,7 +193,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   if (nwin > 1) HIPCHK(c, grow(c, c->idx_win[1], pre + W));
   HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 1)));
   HIPCHK(c, grow(c, c->out, need));
-  HIPCHK(c, grow(c, c->dg_ids, need * 32));
+  if (algo >= 0) HIPCHK(c, grow(c, c->dg_ids, need * 32));
   const int K = dsx_ctx::kIdxSlots;
 
   for (int attempt = 0; attempt < 2; ++attempt) {
@@ -241,6 +241,11 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       }
       // the window's finished chunks: [snap[w].total, snap[w+1].total) from
       // snap[w].carry, all inside this window's bytes
+      if (algo < 0) {  // cut list only (dsx_cut_host / dsx_cut_fd)
+        hipError_t e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
+        if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
+        continue;
+      }
       hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
                          (const DevState*)c->state.p, c->idx_snap.p + 2 * (w + 1));
       DigestArgs da{};
@@ -274,7 +279,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     if (st.total > cap) return DSX_E_CAPACITY;
     if (st.total) {
       HIPCHK(c, hipMemcpy(out_ends, c->out.p, st.total * 8, hipMemcpyDeviceToHost));
-      HIPCHK(c, hipMemcpy(out_ids, c->dg_ids.p, st.total * 32, hipMemcpyDeviceToHost));
+      if (out_ids) HIPCHK(c, hipMemcpy(out_ids, c->dg_ids.p, st.total * 32, hipMemcpyDeviceToHost));
     }
     return DSX_OK;
   }
@@ -316,6 +321,31 @@ extern "C" int dsx_index_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, co
   FdSrc s{fd, off};
   const int rc = run_index(c, p, algo, len, fill_fd, &s, out_ends, ids, cap, n_out);
   c->cancel.store(0);  // a dsx_cancel() issued before or during this call ends here
+  return rc;
+}
+
+// The cut list alone from a file or host memory: the same pipeline without
+// the digests.
+extern "C" int dsx_cut_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, const dsx_params_t* p,
+                          uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
+  if (!c || !p || !n_out || fd < 0 || (cap && !out_ends)) return DSX_E_INVAL;
+  if (len == UINT64_MAX) {
+    const off_t end = lseek(fd, 0, SEEK_END);
+    if (end < 0) return DSX_E_IO;
+    len = (uint64_t)end > off ? (uint64_t)end - off : 0;
+  }
+  FdSrc s{fd, off};
+  const int rc = run_index(c, p, -1, len, fill_fd, &s, out_ends, nullptr, cap, n_out);
+  c->cancel.store(0);
+  return rc;
+}
+
+extern "C" int dsx_cut_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, const dsx_params_t* p,
+                            uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
+  if (!c || !p || !n_out || (len && !h_blob) || (cap && !out_ends)) return DSX_E_INVAL;
+  MemSrc s{(const uint8_t*)h_blob};
+  const int rc = run_index(c, p, -1, len, fill_mem, &s, out_ends, nullptr, cap, n_out);
+  c->cancel.store(0);
   return rc;
 }
 
