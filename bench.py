@@ -45,8 +45,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the cpu_baseline leg (0: the job's CPU share)")
     ap.add_argument("--inflight", type=int, default=3,
-                    help="N=1: chunking jobs kept in flight (one library context each), so "
-                         "the host's wait for job k overlaps the GPU work of job k+1")
+                    help="chunking jobs kept in flight (one library context each), so the "
+                         "host's wait for job k overlaps the GPU work of job k+1 (N > 1: "
+                         "pipeline lanes, one host thread and process group each)")
     ap.add_argument("--check", action="store_true",
                     help="N>1: compare the concatenated per-rank cut lists with one "
                          "dsx_cut_device over the whole blob on rank 0 (small sizes)")
@@ -200,9 +201,18 @@ def main():
     cap = n // MIN + 4
     out = torch.empty(cap, dtype=torch.int64, device="cuda")
     shard = None
+    lanes = []
     if world > 1:
+        # N > 1: `inflight` pipeline lanes, each with its own library context
+        # and process group, run their share of the steps in host threads, so
+        # one lane's host round trips (seam record, RCCL all-gather, resolve)
+        # overlap another lane's kernels
         from desync_amd.shard import DeviceShard
-        shard = DeviceShard(ctx, d_ptr, halo, rank * n, n, n * world, p)
+        for i in range(max(1, args.inflight)):
+            c_i = ctx if i == 0 else _lib.Context(gpu)
+            g_i = None if i == 0 else dist.new_group()
+            lanes.append(DeviceShard(c_i, d_ptr, halo, rank * n, n, n * world, p, group=g_i))
+        shard = lanes[0]
 
     # N = 1: every step is one complete dsx_cut_device job (scan + stitch, cut
     # list in HBM) whose count the host collects.  Jobs rotate over `inflight`
@@ -249,19 +259,48 @@ def main():
                 last = collect(i, record)
         return last
 
-    for s in range(args.warmup):
-        step(s)
-    drain(args.warmup, False)
+    def run_lanes(nsteps):
+        """N > 1: steps s = i, i + L, ... on lane i (one host thread each)."""
+        import threading
+        res, errs = [None] * len(lanes), []
+
+        def lane(i):
+            try:
+                torch.cuda.set_device(gpu)  # (the current device is per thread)
+                for _ in range(i, nsteps, len(lanes)):
+                    res[i] = lanes[i].run()
+            except BaseException as e:  # noqa: BLE001 -- re-raised below
+                errs.append(e)
+
+        ts = [threading.Thread(target=lane, args=(i,)) for i in range(len(lanes))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        return res[0]
+
+    if world == 1:
+        for s in range(args.warmup):
+            step(s)
+        drain(args.warmup, False)
+    else:
+        for ln in lanes:  # every lane once, in order on every rank
+            ln.run()
+        run_lanes(args.warmup)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
     chunks = 0
-    for s in range(args.steps):
-        r = step(s, record=True)
-        chunks = r if r is not None else chunks
     if world == 1:
+        for s in range(args.steps):
+            r = step(s, record=True)
+            chunks = r if r is not None else chunks
         chunks = drain(args.steps, True)
+    else:
+        chunks = run_lanes(args.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -323,7 +362,7 @@ def main():
                 "bytes_per_gpu": n,
                 "chunks": int(chunks),
                 "parallelism": f"range-shard x{world}" if world > 1 else "single GPU",
-                "jobs_in_flight": nctx,
+                "jobs_in_flight": nctx if world == 1 else len(lanes),
             },
         }
         if world == 1 and scan_ms:
