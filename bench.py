@@ -260,17 +260,35 @@ def main():
         return last
 
     def run_lanes(nsteps):
-        """N > 1: steps s = i, i + L, ... on lane i (one host thread each)."""
+        """N > 1: steps s = i, i + L, ... on lane i (one host thread each).  The
+        scans (dsx_shard_local) run concurrently; the exchange/resolve part of
+        each step runs in step order, so every rank issues its collectives in
+        the same order (no cross-communicator deadlock)."""
         import threading
+
+        from desync_amd.shard import seam_protocol
         res, errs = [None] * len(lanes), []
+        turn = {"next": 0}
+        cv = threading.Condition()
 
         def lane(i):
             try:
                 torch.cuda.set_device(gpu)  # (the current device is per thread)
-                for _ in range(i, nsteps, len(lanes)):
-                    res[i] = lanes[i].run()
+                for s in range(i, nsteps, len(lanes)):
+                    rec = lanes[i].local()
+                    with cv:
+                        cv.wait_for(lambda: turn["next"] == s or errs)
+                        if errs:
+                            return
+                        try:
+                            res[i] = seam_protocol(lanes[i], world, rec)
+                        finally:
+                            turn["next"] = s + 1
+                            cv.notify_all()
             except BaseException as e:  # noqa: BLE001 -- re-raised below
-                errs.append(e)
+                with cv:
+                    errs.append(e)
+                    cv.notify_all()
 
         ts = [threading.Thread(target=lane, args=(i,)) for i in range(len(lanes))]
         for t in ts:

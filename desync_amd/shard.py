@@ -71,13 +71,13 @@ def failed_ranks(all_bytes: bytes, world: int):
                               "little") & _lib.DSX_SEAM_ERROR]
 
 
-def seam_protocol(engine, world):
+def seam_protocol(engine, world, rec=None):
     """The exchange / resolve loop (dsx.h, multi-GPU shards).  ``engine``:
     local() -> record; exchange(record) -> all records; failed(all) -> ranks
     with DSX_SEAM_ERROR; resolve(all) -> "ok" | "resync" (raises on a local
     failure); record() -> the (re-walked) record; mark_error(record) ->
     record with DSX_SEAM_ERROR; result() -> this rank's cut list."""
-    rec = engine.local()
+    rec = engine.local() if rec is None else rec
     for _ in range(world + 1):
         allrec = engine.exchange(rec)
         bad = engine.failed(allrec)
