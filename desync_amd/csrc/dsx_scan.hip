@@ -68,6 +68,46 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t
       : "memory");
 }
 
+// One line batch of scanl_kernel: 8 LDS-DMA wave instructions into 8
+// consecutive 1 KiB LDS blocks from lds_base, M0 saved once and stepped by
+// 1 KiB (per-instruction dma16 calls saved and restored M0 around each one:
+// 8 issue slots per instruction instead of 4).
+__device__ __forceinline__ void dma16x8(const u32x4& rsrc, const uint32_t (&vo)[8],
+                                        uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %9\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %10, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %10, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %10, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %10, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %5, %10, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %6, %10, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %7, %10, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %8, %10, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), "v"(vo[6]),
+        "v"(vo[7]), "s"(lds_base), "s"(rsrc)
+      : "memory", "scc");
+}
+
 // L2 prefetch: one dword per lane (buffer_load_dword ... lds) into the first
 // 256 B of a staging slot that the next DMA overwrites (loads retire in issue
 // order, so the real data lands last); the line it touches is in L2/MALL when
@@ -663,14 +703,15 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   auto issue = [&](const u32x4& rsrc, uint32_t sh, uint32_t b) {
     if constexpr (VARIANT == 4) return;
     const uint32_t sb = b * (uint32_t)kLine - sh;  // scalar part
+    uint32_t vo[NI];
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       // the opaque scalar sum keeps LICM from hoisting 8 per-lane offsets
       uint32_t ssum = (uint32_t)i * 8u * S + sb;
       asm volatile("" : "+s"(ssum));
-      const uint32_t vo = (b < NB) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
-      dma16(rsrc, vo, stage_lds + (uint32_t)i * 1024u);
+      vo[i] = (b < NB) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
     }
+    dma16x8(rsrc, vo, stage_lds);
   };
 
   // wave-major first regions: when regions do not fill every wave slot, the
