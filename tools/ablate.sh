@@ -2,6 +2,8 @@
 # Scan ablations (DSX_SCAN_VARIANT: 0 full, 1 no boundary test, 3 staging only,
 # 4 no staging) at 1 and 4 GiB, then SQ/GRBM counters of the full scan.
 set -o pipefail
+# ablation variants are in the diagnostic build (make -C desync_amd/csrc diag)
+export DSX_LIB_PATH=$PWD/desync_amd/libdsx_diag.so
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-abl}
 mkdir -p $OUT

@@ -3,6 +3,8 @@
 # (0 full, 3 staging only, 4 hashing only), 4 GiB uniform.  The clock is
 # GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (kernel trace of the same run).
 set -o pipefail
+# ablation variants are in the diagnostic build (make -C desync_amd/csrc diag)
+export DSX_LIB_PATH=$PWD/desync_amd/libdsx_diag.so
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-clk}
 mkdir -p $OUT
