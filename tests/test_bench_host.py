@@ -1,0 +1,36 @@
+"""bench.py's host-side pieces that need no GPU: the cpu_baseline object of
+the JSON line (the C restatement of the reference's make.go split-and-align,
+timed at the job's CPU share and at n = 10) and its labels."""
+import numpy as np
+
+import bench
+from oracle import oracle as o
+
+
+def test_cpu_baseline_object():
+    blob = o.synth_uniform_c(1, 0, 32 << 20)
+    cb = bench.cpu_baseline(blob, threads=2)
+    assert cb["kind"] == "port" and cb["unit"] == "GiB/s" and cb["cores"] == 2
+    for k in ("value", "n10_gibs", "single_thread_gibs", "ids_sha512_256_gibs"):
+        assert cb[k] > 0, k
+    assert "n=10" in cb["sample"] and "2 threads" in cb["sample"]
+
+
+def test_cpu_share_reads_omp_num_threads(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench.cpu_share() == 16
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert 1 <= bench.cpu_share() <= 16
+
+
+def test_data_labels_name_the_generator_seeds():
+    assert "seed 1" in bench.DATA_LABEL["uniform"]
+    assert "seed 2" in bench.DATA_LABEL["dedup"]
+
+
+def test_cpu_leg_matches_the_sequential_chain():
+    """What the baseline times is the reference's result: split-and-align ==
+    the sequential Next loop (make_test.go:16-80)."""
+    blob = o.synth_uniform_c(2, 0, 8 << 20)
+    assert np.array_equal(o.chunk_parallel(blob, bench.MIN, bench.AVG, bench.MAX, 4),
+                          o.chunk_stream(blob, bench.MIN, bench.AVG, bench.MAX))
