@@ -54,6 +54,7 @@ EXPORTS = (
     "dsx_stream_pop_many", "dsx_stream_window", "dsx_stream_unpop", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host", "dsx_copy",
+    "dsx_ids_fd", "dsx_ids_host",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -170,6 +171,8 @@ def lib():
             "dsx_index_fd": (i32, [vp, i32, u64, u64, P(Params), i32, vp, vp, u64, P(u64)]),
             "dsx_index_host": (i32, [vp, vp, u64, P(Params), i32, vp, vp, u64, P(u64)]),
             "dsx_debug_trace": (i32, [vp, vp, u64, P(u64), P(u64)]),
+            "dsx_ids_fd": (i32, [vp, i32, u64, u64, u64, vp, u64, i32, vp]),
+            "dsx_ids_host": (i32, [vp, vp, u64, u64, vp, u64, i32, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -287,6 +287,114 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   return DSX_E_INTERNAL;
 }
 
+// IDs of a given contiguous chunk list [start, ends[0]), [ends[0], ends[1]),
+// ... of the source's bytes [0, len): the same reader / window pipeline as
+// run_index without the scan.  The source is read from `start` to the last
+// end; a window's halo is the longest chunk, so every chunk is hashed in the
+// window where it ends, with all its bytes resident.  The ranges per window
+// come from the host's list (no device snapshots).
+int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t start,
+            const uint64_t* ends, uint64_t n, uint8_t* out_ids) {
+  HIPCHK(c, hipSetDevice(c->device));
+  c->err.clear();
+  if (n == 0) return DSX_OK;
+  if (n > 0xFFFFFFF0ull) return DSX_E_INVAL;
+  uint64_t prev = start, maxc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (ends[i] < prev || ends[i] > len) {
+      c->err = "chunk ends must be non-decreasing, start <= ends[0], ends[n-1] <= len";
+      return DSX_E_INVAL;
+    }
+    maxc = std::max(maxc, ends[i] - prev);
+    prev = ends[i];
+  }
+  // bytes [start, last) relative to `start` from here on
+  const uint64_t L = ends[n - 1] - start;
+  const uint64_t pre = (maxc + kLine - 1) / kLine * kLine;
+  uint64_t piece = std::min<uint64_t>(c->index_slot, std::max<uint64_t>(L, 4096));
+  piece = (piece + 4095) & ~4095ull;
+  uint64_t W = std::max<uint64_t>(c->index_window, 2 * pre);
+  W = (W + piece - 1) / piece * piece;
+  if (W >= L) W = std::max<uint64_t>(piece, (L + piece - 1) / piece * piece);  // one window
+  const uint64_t nwin = std::max<uint64_t>(1, (L + W - 1) / W);
+  int rc = index_setup(c, piece);
+  if (rc) return rc;
+  HIPCHK(c, grow(c, c->idx_win[0], pre + W));
+  if (nwin > 1) HIPCHK(c, grow(c, c->idx_win[1], pre + W));
+  HIPCHK(c, grow(c, c->dg_ends, n));
+  HIPCHK(c, grow(c, c->dg_ids, n * 32));
+  // the list, relative to `start`, on the device
+  {
+    std::vector<uint64_t> rel(n);
+    for (uint64_t i = 0; i < n; ++i) rel[i] = ends[i] - start;
+    HIPCHK(c, hipMemcpyAsync(c->dg_ends.p, rel.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  struct Shifted {
+    FillFn fill;
+    void* ud;
+    uint64_t start;
+  } sh{fill, ud, start};
+  auto fill_shifted = [](void* u, uint8_t* dst, uint64_t off, uint64_t cnt) {
+    const Shifted* s = (const Shifted*)u;
+    return s->fill(s->ud, dst, s->start + off, cnt);
+  };
+  const int K = dsx_ctx::kIdxSlots;
+  Prefetcher pf(fill_shifted, &sh, L, piece, c->idx_slots, K, c->index_readers);
+  uint64_t k = 0, i0 = 0;
+  for (uint64_t w = 0; w < nwin; ++w) {
+    const uint64_t ws = w * W, wl = std::min(W, L - ws);
+    uint8_t* buf = c->idx_win[w & 1].p;
+    if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
+    if (w >= 1)
+      HIPCHK(c, hipMemcpyAsync(buf, c->idx_win[(w - 1) & 1].p + W, pre, hipMemcpyDeviceToDevice,
+                               c->copy_stream));
+    for (uint64_t off = ws; off < ws + wl; off += piece, ++k) {
+      if (c->cancel.load()) return drain(c, pf, DSX_E_INTERRUPTED);
+      uint8_t* hp = nullptr;
+      uint64_t hn = 0;
+      rc = pf.wait(k, &hp, &hn);
+      if (rc) return drain(c, pf, rc);
+      hipError_t e = hipMemcpyAsync(buf + pre + (off - ws), hp, hn, hipMemcpyHostToDevice,
+                                    c->copy_stream);
+      if (e == hipSuccess) e = hipEventRecord(c->idx_copy_ev[k % K], c->copy_stream);
+      if (e == hipSuccess && k >= 1) e = hipEventSynchronize(c->idx_copy_ev[(k - 1) % K]);
+      if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: H2D"));
+      if (k >= 1) pf.release(k - 1);
+    }
+    // chunks ending in (ws, ws + wl] (window 0 also those ending at 0)
+    uint64_t i1 = i0;
+    while (i1 < n && ends[i1] - start <= ws + wl) ++i1;
+    if (w + 1 == nwin) i1 = n;
+    if (i1 > i0) {
+      hipError_t e = hipSuccess;
+      if (k >= 1) e = hipStreamWaitEvent(c->stream, c->idx_copy_ev[(k - 1) % K], 0);
+      if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: wait"));
+      DigestArgs da{};
+      da.blob = w == 0 ? buf + pre : buf;
+      da.base_off = w == 0 ? 0 : ws - pre;
+      da.len = w == 0 ? wl : pre + wl;
+      da.ends = c->dg_ends.p + i0;
+      da.first_start = i0 == 0 ? 0 : ends[i0 - 1] - start;
+      da.n = i1 - i0;
+      da.ids = c->dg_ids.p + i0 * 32;
+      rc = launch_digest(c, da, i1 - i0, algo);
+      if (rc) return drain(c, pf, rc);
+    } else if (k >= 1) {  // (the window's buffer is free once its copies landed)
+      hipError_t e = hipStreamWaitEvent(c->stream, c->idx_copy_ev[(k - 1) % K], 0);
+      if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: wait"));
+    }
+    hipError_t e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
+    if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: record"));
+    i0 = i1;
+  }
+  pf.stop();
+  HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+  HIPCHK(c, hipMemcpyAsync(out_ids, c->dg_ids.p, n * 32, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return DSX_OK;
+}
+
 }  // namespace
 
 void index_release(dsx_ctx* c) {
@@ -356,6 +464,32 @@ extern "C" int dsx_index_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, co
     return DSX_E_INVAL;
   MemSrc s{(const uint8_t*)h_blob};
   const int rc = run_index(c, p, algo, len, fill_mem, &s, out_ends, ids, cap, n_out);
+  c->cancel.store(0);
+  return rc;
+}
+
+// IDs of a given chunk list read from a file / host memory (VerifyIndex,
+// verifyindex.go:13-79; ChopFile's NewChunkWithID check, chop.go:76-80,
+// chunk.go:60-73).
+extern "C" int dsx_ids_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, uint64_t start,
+                          const uint64_t* ends, uint64_t n, int algo, uint8_t* ids) {
+  if (!c || fd < 0 || (n && (!ends || !ids)) || bad_algo(algo)) return DSX_E_INVAL;
+  if (len == UINT64_MAX) {
+    const off_t end = lseek(fd, 0, SEEK_END);
+    if (end < 0) return DSX_E_IO;
+    len = (uint64_t)end > off ? (uint64_t)end - off : 0;
+  }
+  FdSrc s{fd, off};
+  const int rc = run_ids(c, algo, len, fill_fd, &s, start, ends, n, ids);
+  c->cancel.store(0);
+  return rc;
+}
+
+extern "C" int dsx_ids_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, uint64_t start,
+                            const uint64_t* ends, uint64_t n, int algo, uint8_t* ids) {
+  if (!c || (len && !h_blob) || (n && (!ends || !ids)) || bad_algo(algo)) return DSX_E_INVAL;
+  MemSrc s{(const uint8_t*)h_blob};
+  const int rc = run_ids(c, algo, len, fill_mem, &s, start, ends, n, ids);
   c->cancel.store(0);
   return rc;
 }

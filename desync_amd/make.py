@@ -16,7 +16,6 @@ from __future__ import annotations
 import ctypes
 import os
 import stat as _stat
-import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -50,6 +49,9 @@ class NullProgressBar:
         pass
 
     def Add(self, n):
+        pass
+
+    def Increment(self):
         pass
 
     def Finish(self):
@@ -134,73 +136,6 @@ def chunk_ids(ptr, length, ends, start=0, ctx=None, algo=None):
         check(lib().dsx_chunk_ids(ctx.h, ctypes.c_void_p(ptr), length, start, ends.ctypes.data,
                                   ends.size, out.ctypes.data, 0, algo), ctx.h)
     return [bytes(r) for r in out]
-
-
-_PIECE = 64 << 20   # bytes per pinned staging slot
-_SLOTS = 4          # slots in flight (reads of one overlap the H2D of the others)
-_staging = {}       # device -> list of pinned host tensors, reused across calls
-_staging_lock = threading.Lock()
-
-
-def _file_to_device(f, size, device):
-    """The whole file in HBM (288 GB per MI355X), for VerifyIndex.  Pieces of
-    64 MiB are read with os.preadv by a small thread pool (the GIL is
-    released) into a ring of pinned slots and copied to the device
-    asynchronously on a side stream, so page-cache reads and the PCIe transfer
-    overlap.  The pinned slots are shared per device under a lock; the side
-    stream first waits for the current stream (the caching allocator may hand
-    back memory that queued work still uses), and is drained before the slots
-    or the tensor are released, also when a read fails."""
-    import concurrent.futures as cf
-
-    import torch
-    dev = torch.device(f"cuda:{device}")
-    t = torch.empty(max(size, 1), dtype=torch.uint8, device=dev)
-    if size == 0:
-        return t
-    fd = f.fileno()
-    npieces = (size + _PIECE - 1) // _PIECE
-    with _staging_lock:
-        slots = _staging.get(device)
-        if slots is None:
-            slots = [torch.empty(_PIECE, dtype=torch.uint8).pin_memory() for _ in range(_SLOTS)]
-            _staging[device] = slots
-
-        def read(k):
-            off = k * _PIECE
-            n = min(_PIECE, size - off)
-            mv = memoryview(slots[k % _SLOTS].numpy())[:n]
-            got = 0
-            while got < n:
-                r = os.preadv(fd, [mv[got:]], off + got)
-                if r <= 0:
-                    raise OSError(f"short read at offset {off + got}")
-                got += r
-            return n
-
-        stream = torch.cuda.Stream(device=dev)
-        stream.wait_stream(torch.cuda.current_stream(dev))
-        try:
-            with cf.ThreadPoolExecutor(max_workers=_SLOTS) as pool:
-                futs = {k: pool.submit(read, k) for k in range(min(_SLOTS, npieces))}
-                try:
-                    for k in range(npieces):
-                        n = futs.pop(k).result()
-                        with torch.cuda.stream(stream):
-                            t[k * _PIECE:k * _PIECE + n].copy_(slots[k % _SLOTS][:n],
-                                                              non_blocking=True)
-                            ev = torch.cuda.Event()
-                            ev.record(stream)
-                        if k + _SLOTS < npieces:
-                            ev.synchronize()  # the slot is free once its copy has landed
-                            futs[k + _SLOTS] = pool.submit(read, k + _SLOTS)
-                finally:
-                    for fu in futs.values():  # (an error: let pending reads finish)
-                        fu.cancel()
-        finally:
-            stream.synchronize()
-        torch.cuda.current_stream(dev).wait_stream(stream)
-    return t
 
 
 def file_size(fd):
@@ -300,6 +235,46 @@ def index_host(data, min_size, avg_size, max_size, algo=None, ctx=None, device=0
     return ends[:n.value].copy(), ids[:n.value].copy()
 
 
+def _ids_call(fn, start, ends, algo, ctx, device, cancel=None):
+    code = _digest_code(algo)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    ids = np.empty((ends.size, 32), dtype=np.uint8)
+
+    def call(c):
+        with _CancelWatch(cancel, c):
+            rc = fn(c, code, ends, ids)
+        if rc == _lib.DSX_E_INTERRUPTED:
+            raise Interrupted()
+        check(rc, c.h)
+
+    if ends.size:
+        if ctx is not None:
+            call(ctx)
+        else:
+            with _lib.pooled_context(device) as c:
+                call(c)
+    return ids
+
+
+def ids_fd(fd, start, ends, offset=0, length=None, algo=None, ctx=None, device=0, cancel=None):
+    """dsx_ids_fd: Digest.Sum of the chunks [start, ends[0]), [ends[0], ends[1]),
+    ... of a file range (offsets relative to ``offset``), read through the
+    pinned pipeline into HBM and hashed there.  Returns an (n, 32) uint8 array."""
+    size = length if length is not None else 0xFFFFFFFFFFFFFFFF
+    return _ids_call(lambda c, code, e, out: lib().dsx_ids_fd(
+        c.h, fd, offset, size, start, e.ctypes.data, e.size, code, out.ctypes.data),
+        start, ends, algo, ctx, device, cancel)
+
+
+def ids_host(data, start, ends, algo=None, ctx=None, device=0):
+    """dsx_ids_host: as ids_fd for a host-memory blob."""
+    arr = np.ascontiguousarray(np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+                               if not isinstance(data, np.ndarray) else data, dtype=np.uint8)
+    return _ids_call(lambda c, code, e, out: lib().dsx_ids_host(
+        c.h, arr.ctypes.data, arr.size, start, e.ctypes.data, e.size, code, out.ctypes.data),
+        start, ends, algo, ctx, device)
+
+
 class _nullctx:
     def __init__(self, v):
         self.v = v
@@ -375,11 +350,10 @@ def VerifyIndex(ctx, name, idx, n=1, pb=None, device=0):
     fileSeedSegment.Validate does (fileseed.go:183-196).
 
     The reference reads every chunk with ReadAt over ``n`` worker file handles;
-    here the file is read into HBM once and all IDs are computed by
-    dsx_chunk_ids (one launch per contiguous run of chunks).  ``n`` has no
-    effect on the result.  Block/char devices skip the size check
-    (verifyindex.go:26, isDevice)."""
-    import stat as _stat
+    here one library call per contiguous run of chunks (dsx_ids_fd) streams
+    the run's bytes through pinned memory into HBM and hashes every chunk
+    there.  ``n`` has no effect on the result.  Block/char devices skip the
+    size check (verifyindex.go:26, isDevice)."""
     pb = pb or NullProgressBar()
     pb.SetTotal(len(idx.Chunks))
     pb.Start()
@@ -388,29 +362,25 @@ def VerifyIndex(ctx, name, idx, n=1, pb=None, device=0):
         is_dev = _stat.S_ISBLK(st.st_mode) or _stat.S_ISCHR(st.st_mode)
         if not is_dev and st.st_size != idx.Length():
             raise VerifyError(f"index size ({idx.Length()}) does not match file size ({st.st_size})")
-        if ctx is not None and getattr(ctx, "done", lambda: False)():
-            return None  # the reference stops feeding workers and returns g.Wait()
         if not idx.Chunks:
             return None
-        need = max(c.Start + c.Size for c in idx.Chunks)
         with open(name, "rb") as f:
-            size = os.fstat(f.fileno()).st_size if not is_dev else need
-            if need > size:
-                # ReadAt past the end of the file: io.EOF (fileseed.go:187)
-                raise EOFError("EOF")
-            dctx = _lib.default_context(device)
-            blob = _file_to_device(f, need, device)
-        for run in _contiguous_runs(idx.Chunks):
-            if ctx is not None and getattr(ctx, "done", lambda: False)():
-                break
-            start = run[0].Start
-            ends = np.fromiter((c.Start + c.Size for c in run), dtype=np.uint64, count=len(run))
-            ids = chunk_ids(blob.data_ptr(), need, ends, start, ctx=dctx)
-            for c, got in zip(run, ids):
-                if got != bytes(c.ID):
-                    raise VerifyError(f"seed index for {name} doesn't match its data")
-            pb.Add(len(run))
-        del blob
+            size = file_size(f.fileno())
+            if _stat.S_ISCHR(st.st_mode):  # (no size: read what the index covers)
+                size = max(c.Start + c.Size for c in idx.Chunks)
+            for run in _contiguous_runs(idx.Chunks):
+                if ctx is not None and getattr(ctx, "done", lambda: False)():
+                    break  # the reference stops feeding workers and returns g.Wait()
+                start = run[0].Start
+                ends = np.fromiter((c.Start + c.Size for c in run), dtype=np.uint64, count=len(run))
+                if int(ends.max()) > size:
+                    # ReadAt past the end of the file: io.EOF (fileseed.go:187)
+                    raise EOFError("EOF")
+                ids = ids_fd(f.fileno(), start, ends, 0, size, device=device)
+                for c, got in zip(run, ids):
+                    if got.tobytes() != bytes(c.ID):
+                        raise VerifyError(f"seed index for {name} doesn't match its data")
+                pb.Add(len(run))
     finally:
         pb.Finish()
     return None

@@ -304,6 +304,22 @@ int dsx_index_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, const dsx_p
 int dsx_index_host(dsx_ctx_t *ctx, const void *h_blob, uint64_t len, const dsx_params_t *p,
                    int algo, uint64_t *out_ends, uint8_t *ids, uint64_t cap, uint64_t *n_out);
 
+/* ---- chunk IDs of a given chunk list from a file or host memory --------------
+ * Digest.Sum of the chunks [start, ends[0]), [ends[0], ends[1]), ... of the
+ * bytes [off, off+len) of fd (len == UINT64_MAX: to the end) or of
+ * h_blob[0..len): the re-hash of VerifyIndex (verifyindex.go:13-79,
+ * fileseed.go:183-196) and of ChopFile's NewChunkWithID check (chop.go:66-80,
+ * chunk.go:37-73).  Offsets are relative to off; ends must be non-decreasing
+ * with start <= ends[0] and ends[n-1] <= len (else DSX_E_INVAL).  The same
+ * pipeline as dsx_index_fd without the scan: only [start, ends[n-1]) is read,
+ * through pinned staging into two alternating HBM windows whose overlap is the
+ * longest chunk.  ids: n * 32 bytes, host memory.  A file shorter than
+ * ends[n-1] gives DSX_E_IO.  Synchronous; dsx_cancel() interrupts it. */
+int dsx_ids_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, uint64_t start,
+               const uint64_t *ends, uint64_t n, int algo, uint8_t *ids);
+int dsx_ids_host(dsx_ctx_t *ctx, const void *h_blob, uint64_t len, uint64_t start,
+                 const uint64_t *ends, uint64_t n, int algo, uint8_t *ids);
+
 /* ---- statistics (ChunkingStats, make.go:329-341 + scan/stitch timings) ------ */
 typedef struct dsx_stats {
     uint64_t chunks;            /* ChunksAccepted */

@@ -5,7 +5,9 @@ tests/test_gpu_index.py; it must never import torch.
 For each (input, golden caibx) pair it calls dsx_index_fd (file -> cut list
 + SHA-512/256 chunk IDs, all on the GPU), writes the caibx bytes the way
 Index.WriteTo does (index.go:90-124, format.go:582-620; flags as in
-IndexFromFile, make.go:35-62) and compares them with the golden file.
+IndexFromFile, make.go:35-62) and compares them with the golden file; then
+re-hashes the golden table's own chunk list with dsx_ids_fd (VerifyIndex's
+data path, verifyindex.go:13-79) and compares the IDs with the table's.
 Prints "ok <n>" per file; exits non-zero on a mismatch.
 """
 import ctypes
@@ -50,6 +52,7 @@ def main():
     L.dsx_last_error.argtypes = [vp]
     L.dsx_index_fd.argtypes = [vp, ctypes.c_int, u64, u64, ctypes.POINTER(Params), ctypes.c_int,
                                vp, vp, u64, ctypes.POINTER(u64)]
+    L.dsx_ids_fd.argtypes = [vp, ctypes.c_int, u64, u64, u64, vp, u64, ctypes.c_int, vp]
     ctx = vp()
     assert L.dsx_ctx_create(0, ctypes.byref(ctx)) == 0, L.dsx_last_error(None)
     pairs = [("chunker.input", "chunker.index"), ("blob1", "blob1.caibx"), ("blob2", "blob2.caibx"),
@@ -75,12 +78,23 @@ def main():
             n = u64()
             rc = L.dsx_index_fd(ctx, fd, 0, 0xFFFFFFFFFFFFFFFF, ctypes.byref(p), 0, ends, ids, cap,
                                 ctypes.byref(n))
+            # VerifyIndex's re-hash (dsx_ids_fd) over the golden table's own
+            # chunk list: items of 40 bytes {end offset, ID} after 64 header bytes
+            nt = (len(want) - 64 - 40) // 40
+            gends = (u64 * nt)(*[struct.unpack_from("<Q", want, 64 + 40 * i)[0] for i in range(nt)])
+            gids = [want[64 + 40 * i + 8:64 + 40 * i + 40] for i in range(nt)]
+            vids = (ctypes.c_uint8 * (32 * max(nt, 1)))()
+            vrc = L.dsx_ids_fd(ctx, fd, 0, 0xFFFFFFFFFFFFFFFF, 0, gends, nt, 0, vids)
         finally:
             os.close(fd)
         assert rc == 0, (rc, L.dsx_last_error(ctx))
         got = caibx(flags, mn, av, mx, list(ends[:n.value]),
                     [bytes(ids[32 * i:32 * i + 32]) for i in range(n.value)])
-        if got != want:
+        assert vrc == 0, (vrc, L.dsx_last_error(ctx))
+        if [bytes(vids[32 * i:32 * i + 32]) for i in range(nt)] != gids:
+            bad += 1
+            print("IDS MISMATCH", inp)
+        elif got != want:
             bad += 1
             print("MISMATCH", inp)
         else:

@@ -268,3 +268,151 @@ def test_chunk_stream_errors():
                                                                  AVG, MAX), desync_amd.MemoryStore(), 2)
     ref = o.chunk_stream(data, MIN, AVG, MAX)
     assert [ch.Start + ch.Size for ch in idx.Chunks] == ref[:5].tolist()
+
+
+# ------------------------------------------------- dsx_ids_fd / dsx_ids_host
+@pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
+def test_ids_fd_many_windows(tmp_path, monkeypatch, algo):
+    """The re-hash of a given chunk list (VerifyIndex / ChopFile) through 1 MiB
+    HBM windows and 256 KiB read slots: the oracle's cut list of 24 MiB from a
+    non-zero start, a file range at an offset, a 3 MiB chunk (longer than a
+    window: the window overlap grows to it) and zero-length chunks; every ID
+    against hashlib, fd and host paths alike."""
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_INDEX_WINDOW", str(1 << 20))
+    monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 18))
+    data = o.synth_uniform(48, 0, (24 << 20) + 4321)
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ctx = _lib.Context(0)
+    fd = os.open(str(f), os.O_RDONLY)
+    try:
+        start = int(ref[3])
+        ends = ref[4:]
+        want = _ids(data[start:], ends - start, algo)
+        got = desync_amd.ids_fd(fd, start, ends, algo=algo, ctx=ctx)
+        assert [bytes(x) for x in got] == want
+        got = desync_amd.ids_host(data, start, ends, algo=algo, ctx=ctx)
+        assert [bytes(x) for x in got] == want
+        # a range of the file at an offset: offsets relative to it
+        off = 777
+        sub = data[off:off + (9 << 20)]
+        e2 = np.array([5, 5, 5 + (3 << 20), (3 << 20) + 70000, (3 << 20) + 70000, sub.size], np.uint64)
+        got = desync_amd.ids_fd(fd, 5, e2, offset=off, length=sub.size, algo=algo, ctx=ctx)
+        assert [bytes(x) for x in got] == _ids(sub[5:], e2 - 5, algo)
+        # one chunk: the whole file; no chunks
+        got = desync_amd.ids_fd(fd, 0, np.array([data.size], np.uint64), algo=algo, ctx=ctx)
+        assert bytes(got[0]) == _ids(data, np.array([data.size], np.uint64), algo)[0]
+        assert desync_amd.ids_fd(fd, 0, np.array([], np.uint64), ctx=ctx).shape == (0, 32)
+    finally:
+        os.close(fd)
+        ctx.close()
+
+
+def test_ids_fd_errors(tmp_path):
+    """Malformed chunk lists are rejected before any read (DSX_E_INVAL); a
+    list past the end of the file gives DSX_E_IO; the context keeps working."""
+    import desync_amd
+    from desync_amd import _lib
+    data = o.synth_uniform(49, 0, 1 << 20)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ctx = _lib.Context(0)
+    fd = os.open(str(f), os.O_RDONLY)
+    try:
+        for start, ends in ((0, [100, 50]), (200, [100, 300]), (0, [100, data.size + 1])):
+            with pytest.raises(_lib.DsxError) as ei:
+                desync_amd.ids_fd(fd, start, np.array(ends, np.uint64), length=data.size, ctx=ctx)
+            assert ei.value.code == _lib.DSX_E_INVAL, (start, ends)
+        with pytest.raises(_lib.DsxError) as ei:
+            desync_amd.ids_fd(fd, 0, np.array([100, data.size + 4096], np.uint64),
+                              length=data.size + 4096, ctx=ctx)
+        assert ei.value.code == _lib.DSX_E_IO
+        got = desync_amd.ids_fd(fd, 0, np.array([100, data.size], np.uint64), ctx=ctx)
+        assert [bytes(x) for x in got] == _ids(data, np.array([100, data.size], np.uint64))
+    finally:
+        os.close(fd)
+        ctx.close()
+
+
+# ------------------------------------------------------------------- ChopFile
+class _Count:
+    def __init__(self):
+        self.total, self.inc, self.finished = None, 0, False
+
+    def SetTotal(self, n):
+        self.total = n
+
+    def Start(self):
+        pass
+
+    def Increment(self):
+        self.inc += 1
+
+    def Finish(self):
+        self.finished = True
+
+
+def test_chop_file_golden(tmp_path, golden):
+    """chop.go:14-81 over testdata/chunker.input with its golden index: every
+    chunk stored once under its ID with its exact bytes; a wrong ID raises
+    ChunkInvalid with errors.go's message; a truncated file raises EOFError;
+    a store error is raised."""
+    import desync_amd
+    f = tmp_path / "chunker.input"
+    raw = golden("chunker.input")
+    f.write_bytes(raw)
+    idx = desync_amd.IndexFromReader(golden("chunker.index"))
+    store, pb = desync_amd.MemoryStore(), _Count()
+    assert desync_amd.ChopFile(None, str(f), idx.Chunks, store, 4, pb) is None
+    assert pb.total == pb.inc == len(idx.Chunks) == 20 and pb.finished
+    assert sorted(store.chunks) == sorted(bytes(c.ID) for c in idx.Chunks)
+    for c in idx.Chunks:
+        assert store.chunks[bytes(c.ID)] == raw[c.Start:c.Start + c.Size]
+
+    bad = list(idx.Chunks)
+    k = 7
+    bad[k] = desync_amd.IndexChunk(bytes(32), bad[k].Start, bad[k].Size)
+    with pytest.raises(desync_amd.ChunkInvalid) as ei:
+        desync_amd.ChopFile(None, str(f), bad, desync_amd.MemoryStore(), 2)
+    want_sum = hashlib.new("sha512_256", raw[bad[k].Start:bad[k].Start + bad[k].Size]).digest()
+    assert str(ei.value) == f"chunk id {'00' * 32} does not match its hash {want_sum.hex()}"
+
+    short = tmp_path / "short"
+    short.write_bytes(raw[:idx.Chunks[-3].Start + 10])
+    with pytest.raises(EOFError):
+        desync_amd.ChopFile(None, str(short), idx.Chunks, desync_amd.MemoryStore(), 3)
+
+    class Bad(desync_amd.MemoryStore):
+        def StoreChunk(self, chunk):
+            raise IOError("store down")
+
+    with pytest.raises(IOError, match="store down"):
+        desync_amd.ChopFile(None, str(f), idx.Chunks, Bad(), 2)
+
+
+def test_chop_file_large_sha256(tmp_path):
+    """IndexFromFile -> ChopFile over 64 MiB with repeated blocks, SHA-256:
+    the store holds each distinct chunk once with its bytes."""
+    import desync_amd
+    from desync_amd import digest
+    blk = o.synth_uniform(50, 0, 4 << 20)
+    data = np.concatenate([o.synth_uniform(51, 0, 30 << 20), blk, o.synth_uniform(52, 0, 20 << 20),
+                           blk, np.zeros(2 << 20, np.uint8), blk])
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    prev = digest.Digest.Algorithm()
+    desync_amd.set_digest("sha256")
+    try:
+        idx, _ = desync_amd.IndexFromFile(None, str(f), 4, MIN, AVG, MAX)
+        store = desync_amd.MemoryStore()
+        desync_amd.ChopFile(None, str(f), idx.Chunks, store, 8)
+    finally:
+        desync_amd.set_digest(prev)
+    raw = data.tobytes()
+    assert len(store.chunks) == len({bytes(c.ID) for c in idx.Chunks}) < len(idx.Chunks)
+    for c in idx.Chunks[::37]:
+        assert store.chunks[bytes(c.ID)] == raw[c.Start:c.Start + c.Size]
+        assert hashlib.sha256(raw[c.Start:c.Start + c.Size]).digest() == bytes(c.ID)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """End-to-end `desync make` rate (IndexFromFile, make.go:22-163): a file in
 the page cache -> HBM -> cut list -> chunk IDs (SHA-512/256) -> Index, plus
-the caibx bytes (Index.WriteTo).  The file is seeded uniform bytes written to
+the caibx bytes (Index.WriteTo); then VerifyIndex of the same index
+(verifyindex.go:13-79: the chunk list re-hashed through dsx_ids_fd).  The file is seeded uniform bytes written to
 $TMPDIR; the cut list is checked against dsx_cut_host on the same bytes and
 three chunk IDs with hashlib.
 
@@ -52,6 +53,10 @@ def main():
                 dt_c = time.perf_counter() - t1
             finally:
                 os.close(fdr)
+            # VerifyIndex over the index just made (dsx_ids_fd: file -> HBM -> IDs)
+            t2 = time.perf_counter()
+            desync_amd.VerifyIndex(None, path, index, 1)
+            dt_v = time.perf_counter() - t2
             raw = np.fromfile(path, dtype=np.uint8)
             want = desync_amd.cut_host(raw, MIN, AVG, MAX)
             got = np.array([c.Start + c.Size for c in index.Chunks], dtype=np.uint64)
@@ -62,11 +67,12 @@ def main():
             del raw
             rows.append({"gib": gib, "chunks": stats.ChunksAccepted, "caibx_bytes": len(b.getvalue()),
                          "s": round(dt, 4), "gibs": round(gib / dt, 2),
-                         "index_fd_s": round(dt_c, 4), "index_fd_gibs": round(gib / dt_c, 2)})
+                         "index_fd_s": round(dt_c, 4), "index_fd_gibs": round(gib / dt_c, 2),
+                         "verify_s": round(dt_v, 4), "verify_gibs": round(gib / dt_v, 2)})
         finally:
             os.unlink(path)
     print(json.dumps({"tool": "make_rate", "params": "16/64/256 KiB", "digest": "sha512-256",
-                      "rows": rows, "note": "page-cache file -> HBM -> cuts + IDs -> caibx bytes (IndexFromFile); index_fd = the C call alone (dsx_index_fd)"}))
+                      "rows": rows, "note": "page-cache file -> HBM -> cuts + IDs -> caibx bytes (IndexFromFile); index_fd = the C call alone (dsx_index_fd); verify = VerifyIndex of that index (dsx_ids_fd)"}))
 
 
 if __name__ == "__main__":
