@@ -174,6 +174,17 @@ __device__ __forceinline__ bool is_cand(uint32_t h, const TestConsts& tc) {
   }
 }
 
+// LDS address of byte k (0..3) of w in the replicated table: byte << 8 |
+// slot8.  Byte 1 already sits at bits 8..15, so (w & 0xFF00) | slot8 is one
+// v_bitop3_b32, which gfx950 issues at the full VALU rate (2.7 cycles per wave64
+// instruction at 4 waves per SIMD, tools/ubench_valu.hip); v_perm_b32, needed
+// to move the other bytes, takes 4.3.
+__device__ __forceinline__ uint32_t lookup_addr(uint32_t w, uint32_t slot8, int k) {
+  if (k == 1) return __builtin_amdgcn_bitop3_b32(w, 0xFF00u, slot8, 0xEA);  // (a & b) | c
+  const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)k) << 8);
+  return __builtin_amdgcn_perm(w, slot8, sel);
+}
+
 // Process one 48-byte round of one lane.  `w` holds the round's bytes,
 // `ring[k]` the rotated table value of the byte 48 positions earlier.
 // The 48 bytes run as 48/SUB subgroups; the table lookups of subgroup j+1 are
@@ -631,24 +642,6 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     for (int e = threadIdx.x; e < W * STG / 4; e += NT)
       reinterpret_cast<uint32_t*>(lds + kTableBytes)[e] = 0u;
   }
-  // one table load per thread (a loop of dependent loads cost ~15 us of the
-  // launch): thread t writes byte value t % 256 into slots of its share
-  {
-    static_assert(NT % 256 == 0, "table fill shape");
-    constexpr int TPV = NT / 256;  // threads per byte value
-    const uint32_t v = threadIdx.x & 255u;
-    const uint32_t tv = kT[v];
-    uint2 t;
-    t.x = tv;
-    t.y = __builtin_amdgcn_alignbit(tv, tv, 16);
-#pragma unroll
-    for (int k = 0; k < (32 + TPV - 1) / TPV; ++k) {
-      const uint32_t slot = (threadIdx.x >> 8) + (uint32_t)(k * TPV);
-      if (slot < 32u) *reinterpret_cast<uint2*>(lds + v * 256u + slot * 8u) = t;
-    }
-  }
-  if (kBal && threadIdx.x < W) s_prog[threadIdx.x] = 0u;
-  __syncthreads();
 
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
@@ -718,19 +711,42 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // idle slots are single waves spread over many CUs (whose partner wave then
   // runs alone, faster) instead of whole CUs at the end of the grid
   uint32_t region = a.wave_major ? wave * gridDim.x + blockIdx.x : blockIdx.x * W + wave;
-  if (region >= a.nregions) return;
+  const bool live = region < a.nregions;
+  // The first line's DMA is issued before the table fill, so its HBM latency
+  // overlaps the fill instead of following it.
+  u32x4 rsrc = {0u, 0u, 0u, 0u};
+  uint32_t sh = 0;
+  uint32_t ticket = 0;
+  if (live) {
+    desc_of(region, rsrc, sh);
+    if (lane == 0) ticket = atomicAdd(a.queue, 1u);
+    issue(rsrc, sh, 0u);
+  }
+  // one table load per thread (a loop of dependent loads cost ~15 us of the
+  // launch): thread t writes byte value t % 256 into slots of its share
+  {
+    static_assert(NT % 256 == 0, "table fill shape");
+    constexpr int TPV = NT / 256;  // threads per byte value
+    const uint32_t v = threadIdx.x & 255u;
+    const uint32_t tv = kT[v];
+    uint2 t;
+    t.x = tv;
+    t.y = __builtin_amdgcn_alignbit(tv, tv, 16);
+#pragma unroll
+    for (int k = 0; k < (32 + TPV - 1) / TPV; ++k) {
+      const uint32_t slot = (threadIdx.x >> 8) + (uint32_t)(k * TPV);
+      if (slot < 32u) *reinterpret_cast<uint2*>(lds + v * 256u + slot * 8u) = t;
+    }
+  }
+  if (kBal && threadIdx.x < W) s_prog[threadIdx.x] = 0u;
+  __syncthreads();
+  if (!live) return;
   // VARIANT 5 (diagnostic, same results): the trace records shader-clock
   // cycles from start to end and those spent waiting for the line DMA
   const uint64_t t_start = VARIANT == 5 ? __builtin_amdgcn_s_memtime()
                                         : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
   uint64_t vm_wait = 0, copy_wait = 0, dma_issue = 0;
   uint32_t nreg_done = 0;
-  u32x4 rsrc;
-  uint32_t sh;
-  desc_of(region, rsrc, sh);
-  uint32_t ticket = 0;
-  if (lane == 0) ticket = atomicAdd(a.queue, 1u);
-  issue(rsrc, sh, 0u);
 
   while (true) {
     const uint32_t next = gridDim.x * W + __builtin_amdgcn_readfirstlane(ticket);
@@ -816,9 +832,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int k = (g % 16) * 8 + q;  // byte within the line
-        const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8);
-        const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot8, sel);
-        L[g % NL][q] = *reinterpret_cast<const uint64_t*>(lds + addr);
+        L[g % NL][q] = *reinterpret_cast<const uint64_t*>(lds + lookup_addr(w[k >> 2], slot8, k & 3));
       }
     };
     auto compute_sub = [&](auto gc, uint32_t o0) __attribute__((always_inline)) {

@@ -295,6 +295,31 @@ def test_periodic_dense_candidates(dctx):
     assert np.array_equal(gpu_cut(dctx, data), o.chunk_stream(data, MIN, AVG, MAX))
 
 
+def test_stitch_many_workgroups_and_repairs(monkeypatch):
+    """The stitch on many walk workgroups (small segments) and on seams inside
+    zero runs (suspect segments: fixup_kernel's sequential repair)."""
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_SEG_FLOOR", "65536")
+    ctx = _lib.Context(0)
+    try:
+        mn, av, mx = 4096, 16384, 65536  # 256 KiB segments: 257 of them, 129 workgroups
+        data = o.synth_uniform(41, 0, (64 << 20) + 4321)
+        assert np.array_equal(gpu_cut(ctx, data, mn, av, mx), o.chunk_stream(data, mn, av, mx))
+        rng = np.random.default_rng(11)
+        null = np.zeros(4 * MAX, np.uint8)
+        r1 = rng.integers(0, 256, 4 * MAX, dtype=np.uint8)
+        # a random head of odd length puts the true chain inside the zero runs
+        # off the segment grid: those seams do not converge (repairs)
+        for parts in ([r1[:12345], null, null, null, r1, null, r1], [null] * 6 + [r1]):
+            d = np.concatenate(parts)
+            assert np.array_equal(gpu_cut(ctx, d), o.chunk_stream(d, MIN, AVG, MAX))
+            if parts[0] is not null:
+                assert ctx.stats().repaired_segments > 0
+            assert np.array_equal(gpu_cut(ctx, d, mn, av, mx), o.chunk_stream(d, mn, av, mx))
+    finally:
+        ctx.close()
+
+
 # ---------------------------------------------------------------- host paths
 def test_host_and_fd_paths(dctx, tmp_path):
     import desync_amd

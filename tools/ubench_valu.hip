@@ -53,6 +53,31 @@ KERNEL(k_lshr, "v_lshrrev_b32 %0, 3, %0")
 KERNEL(k_and, "v_and_b32 %0, %0, %1")
 KERNEL(k_cvt_ubyte, "v_cvt_f32_ubyte1 %0, %0")
 
+
+KERNEL(k_min3f_abs, "v_min3_f32 %0, |%0|, |%1|, |%2|")
+KERNEL(k_minf_abs, "v_min_f32_e64 %0, |%0|, |%1|")
+KERNEL(k_pk_min_u16, "v_pk_min_u16 %0, %0, %1")
+KERNEL(k_max3u, "v_max3_u32 %0, %0, %1, %2")
+KERNEL(k_bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96")
+KERNEL(k_add3, "v_add3_u32 %0, %0, %1, %2")
+KERNEL(k_or, "v_or_b32 %0, %0, %1")
+KERNEL(k_lshl, "v_lshlrev_b32 %0, 3, %0")
+KERNEL(k_mov, "v_mov_b32 %0, %1")
+KERNEL(k_dot2u16, "v_dot2_u32_u16 %0, %0, %1, %2")
+KERNEL(k_madu16, "v_mad_u32_u16 %0, %0, %1, %2")
+KERNEL(k_alignbyte, "v_alignbyte_b32 %0, %0, %1, 1")
+KERNEL(k_mulhi24, "v_mul_hi_u32_u24 %0, %0, %1")
+KERNEL(k_min_u16, "v_min_u16 %0, %0, %1")
+KERNEL(k_pk_mad_u16, "v_pk_mad_u16 %0, %0, %1, %2")
+KERNEL(k_med3u, "v_med3_u32 %0, %0, %1, %2")
+KERNEL(k_minimum3f, "v_minimum3_f32 %0, %0, %1, %2")
+KERNEL(k_min3i, "v_min3_i32 %0, %0, %1, %2")
+KERNEL(k_maxf, "v_max_f32 %0, %0, %1")
+KERNEL(k_addf, "v_add_f32 %0, %0, %1")
+KERNEL(k_sub_f32, "v_sub_f32 %0, %0, %1")
+KERNEL(k_xor_sdwa, "v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2")
+KERNEL(k_lshl_sdwa, "v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2")
+KERNEL(k_and_or, "v_and_or_b32 %0, %0, %1, %2")
 KERNEL(k_lshl_add, "v_lshl_add_u32 %0, %0, 1, %1")
 KERNEL(k_bfe, "v_bfe_u32 %0, %0, 8, 8")
 
@@ -156,9 +181,17 @@ int main() {
             {"v_and_b32", k_and, 8},       {"v_cvt_f32_ubyte1", k_cvt_ubyte, 8},  {"v_pk_fma_f32", k_pkfma, 8},    {"chain alignbit+xor", k_chain, 8},
             {"v_lshl_add_u32", k_lshl_add, 8}, {"v_bfe_u32", k_bfe, 8},
             {"chain1 (alignbit,xor)", k_chainN<1>, 8}, {"chain2", k_chainN<2>, 8}, {"chain4", k_chainN<4>, 8},
-            {"chain8", k_chainN<8>, 8}, {"v_mad_u64_u32", k_mad64, 8}};
+            {"chain8", k_chainN<8>, 8}, {"v_mad_u64_u32", k_mad64, 8},
+            {"v_min3_f32 abs", k_min3f_abs, 8}, {"v_min_f32 abs", k_minf_abs, 8}, {"v_pk_min_u16", k_pk_min_u16, 8},
+            {"v_max3_u32", k_max3u, 8}, {"v_bitop3_b32", k_bitop3, 8}, {"v_add3_u32", k_add3, 8}, {"v_or_b32", k_or, 8},
+            {"v_lshlrev_b32", k_lshl, 8}, {"v_mov_b32", k_mov, 8}, {"v_dot2_u32_u16", k_dot2u16, 8},
+            {"v_mad_u32_u16", k_madu16, 8}, {"v_alignbyte_b32", k_alignbyte, 8}, {"v_mul_hi_u32_u24", k_mulhi24, 8},
+            {"v_min_u16", k_min_u16, 8}, {"v_pk_mad_u16", k_pk_mad_u16, 8}, {"v_med3_u32", k_med3u, 8},
+            {"v_minimum3_f32", k_minimum3f, 8}, {"v_min3_i32", k_min3i, 8}, {"v_max_f32", k_maxf, 8},
+            {"v_add_f32", k_addf, 8}, {"v_sub_f32", k_sub_f32, 8}, {"v_xor_b32_sdwa", k_xor_sdwa, 8},
+            {"v_lshlrev_b32_sdwa", k_lshl_sdwa, 8}, {"v_and_or_b32", k_and_or, 8}};
   printf("clock attr %d kHz\n", clk_khz);
-  for (int wps : {1, 2, 4}) {
+  for (int wps : {2, 4}) {
     for (auto& k : ks) {
       const int threads = 64 * 4 * wps;  // one block per CU, wps waves per SIMD
       hipLaunchKernelGGL(k.f, dim3(ncu), dim3(threads), 0, 0, o, 1u);
