@@ -32,10 +32,12 @@ __device__ __forceinline__ void k_hash(uint32_t* out, uint32_t seed) {
   uint32_t acc = 0;
   const uint32_t ninv = seed | 1u, thr = 7u;
   uint64_t L[2][8];
+  uint64_t L3[3][8];
   uint32_t LT[2][8], LR[2][8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     L[0][q] = L[1][q] = q;
+    L3[0][q] = L3[1][q] = L3[2][q] = q;
     LT[0][q] = LT[1][q] = LR[0][q] = LR[1][q] = q;
   }
   for (int t = 0; t < TRIPS; ++t) {
@@ -58,6 +60,15 @@ __device__ __forceinline__ void k_hash(uint32_t* out, uint32_t seed) {
           const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot8, sel);
           const uint64_t v = L[g & 1][q];
           L[(g + 1) & 1][q] = *reinterpret_cast<const uint64_t*>(lds + addr);
+          x = (uint32_t)v;
+          y = ring[(g * 8 + q) % 48];
+          ring[(g * 8 + q) % 48] = (uint32_t)(v >> 32);
+        } else if constexpr (KIND == 4) {  // lookups two subgroups ahead
+          const int k2 = ((g + 2) % 8) * 8 + q;
+          const uint32_t sel2 = 0x0C0C0000u | ((4u + (uint32_t)(k2 & 3)) << 8);
+          const uint32_t addr = __builtin_amdgcn_perm(w[k2 >> 2], slot8, sel2);
+          const uint64_t v = L3[g % 3][q];
+          L3[(g + 2) % 3][q] = *reinterpret_cast<const uint64_t*>(lds + addr);
           x = (uint32_t)v;
           y = ring[(g * 8 + q) % 48];
           ring[(g * 8 + q) % 48] = (uint32_t)(v >> 32);
@@ -119,5 +130,6 @@ int main() {
   run<1, 1>("mix", d, ncu);   run<1, 2>("mix", d, ncu);   run<1, 3>("mix", d, ncu);   run<1, 4>("mix", d, ncu);
   run<2, 1>("lds", d, ncu);   run<2, 2>("lds", d, ncu);   run<2, 3>("lds", d, ncu);   run<2, 4>("lds", d, ncu);
   run<3, 1>("lds32", d, ncu); run<3, 2>("lds32", d, ncu); run<3, 3>("lds32", d, ncu); run<3, 4>("lds32", d, ncu);
+  run<4, 1>("lds_d2", d, ncu); run<4, 2>("lds_d2", d, ncu); run<4, 3>("lds_d2", d, ncu);
   return 0;
 }
