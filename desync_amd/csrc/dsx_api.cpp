@@ -182,6 +182,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SCAN_TRACE")) c->scan_trace = atoi(v) != 0;
   if (const char* v = getenv("DSX_WAVE_MAJOR")) c->wave_major = atoi(v) != 0;
   if (const char* v = getenv("DSX_FIXUP_FAST")) c->fixup_fast = atoi(v) != 0;
+  if (const char* v = getenv("DSX_FINISH")) c->finish = atoi(v) != 0;
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_LANE_TARGET"))
@@ -588,6 +589,15 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   const size_t walk_lds = (size_t)kWalkLdsCap * 4 + (kMaxSpg + 1) * 8;
   hipLaunchKernelGGL(walk_kernel, dim3(walk_grid), dim3(256), walk_lds, c->stream, ta);
   HIPCHK(c, hipGetLastError());
+  if (c->finish && nseg <= 2048) {  // fixup + gather over nseg/16 workgroups
+    const dim3 fg((uint32_t)((nseg + 15) / 16));
+    if (nseg <= 256) hipLaunchKernelGGL(finish_kernel<1>, fg, dim3(256), 0, c->stream, ta);
+    else if (nseg <= 512) hipLaunchKernelGGL(finish_kernel<2>, fg, dim3(256), 0, c->stream, ta);
+    else if (nseg <= 1024) hipLaunchKernelGGL(finish_kernel<4>, fg, dim3(256), 0, c->stream, ta);
+    else hipLaunchKernelGGL(finish_kernel<8>, fg, dim3(256), 0, c->stream, ta);
+    HIPCHK(c, hipGetLastError());
+    return DSX_OK;
+  }
   if (c->fixup_fast && nseg <= 8 * 1024) {
     if (nseg <= 1024) hipLaunchKernelGGL(fixup_fast_kernel<1>, dim3(1), dim3(1024), 0, c->stream, ta);
     else if (nseg <= 2048) hipLaunchKernelGGL(fixup_fast_kernel<2>, dim3(1), dim3(1024), 0, c->stream, ta);

@@ -28,6 +28,8 @@ __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
 template <int PER>
 __global__ void fixup_fast_kernel(StitchArgs a);
+template <int PER>
+__global__ void finish_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);
 __global__ void state_init_kernel(DevState* st, uint64_t carry);
 __global__ void gen_uniform_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed);
@@ -110,6 +112,7 @@ struct dsx_ctx {
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
   bool wave_major = true;             // DSX_WAVE_MAJOR: scanl's first regions wave-major
+  bool finish = true;                 // DSX_FINISH=0: fixup_fast_kernel + gather_kernel instead of finish_kernel
   bool fixup_fast = true;             // DSX_FIXUP_FAST=0: fixup_kernel for every piece
   DevBuf<uint64_t> trace;       // [3 * trace_n scan records][10 * trace_walk_n walk records]
   uint64_t trace_n = 0, trace_walk_n = 0;

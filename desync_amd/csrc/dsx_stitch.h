@@ -50,6 +50,11 @@ struct DevState {
   uint32_t err;         // kErr* bits
   uint32_t active;      // current piece was processed (K3 ran its body)
   uint32_t pad;
+  // snapshots taken by walk_kernel for finish_kernel, whose workgroups must
+  // not read fields its last workgroup updates
+  uint64_t base;        // total at the start of the piece's stitch
+  uint32_t skip;        // done or overflow at that point
+  uint32_t pad2;
 };
 
 // Published by the last kernel of a piece into pinned host memory.

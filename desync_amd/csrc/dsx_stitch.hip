@@ -265,7 +265,11 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
 
   uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 10ull * blockIdx.x : nullptr;
   if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
-  const DevState* st = a.state;
+  DevState* st = a.state;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // for finish_kernel
+    st->base = st->total;
+    st->skip = (st->done || *a.pc.overflow) ? 1u : 0u;
+  }
   if (st->done || *a.pc.overflow) return;  // finished, or scan lists overflowed
   const uint64_t s0 = uniform64(st->carry);  // scalar: the walks below are wave-uniform
   const uint32_t kA = blockIdx.x * a.spg;
@@ -765,6 +769,186 @@ template __global__ void fixup_fast_kernel<1>(StitchArgs);
 template __global__ void fixup_fast_kernel<2>(StitchArgs);
 template __global__ void fixup_fast_kernel<4>(StitchArgs);
 template __global__ void fixup_fast_kernel<8>(StitchArgs);
+
+// K3 + K4 over many workgroups, for pieces of at most kFinMaxSeg segments:
+// every workgroup loads all the SegInfo (40 B per segment, one round of global
+// loads), checks fixup_kernel's rule (no suspect segment: flagged, or the
+// previous segment's X != Z or flagged) and scans the counts in LDS; then it
+// copies its own 16 segments' staged lists to the output, one wave per
+// segment and one lane per cut (coalesced).  The last workgroup publishes the
+// chain state.  It reads only walk_kernel's snapshots (DevState.base/skip),
+// never a field the last workgroup writes.  With a suspect segment, workgroup
+// 0 runs fixup_kernel's body and the gather alone (rare: a seam that did not
+// converge, dense candidates).  Replaces fixup_fast_kernel + gather_kernel
+// (one launch and a single-workgroup round trip less).
+constexpr int kFinThreads = 256;
+constexpr uint32_t kFinMaxSeg = 2048;  // 8 per thread
+constexpr uint32_t kFinSegPerWg = 16;  // 4 per wave
+
+template <int PER>
+__global__ __launch_bounds__(kFinThreads) void finish_kernel(StitchArgs a) {
+  constexpr int NT = kFinThreads;
+  constexpr uint32_t kBad = kSegDense | kSegOverflow;
+  __shared__ uint64_t s_lx[NT], s_lz[NT];  // X, Z of each thread's last segment
+  __shared__ uint32_t s_lf[NT];            // and its flags
+  __shared__ uint64_t s_off[kFinMaxSeg];   // output offset of every segment
+  __shared__ uint32_t s_cnt[kFinMaxSeg];
+  __shared__ uint64_t s_part[NT / 64];
+  __shared__ int s_last_seg;
+  __shared__ uint64_t s_carry, s_piece;
+  DevState* st = a.state;
+  const uint32_t T = a.nseg;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t k0 = tid * PER;
+  const uint32_t skip = st->skip;
+  const uint64_t base = st->base;
+  uint64_t X[PER], Z[PER];
+  uint32_t cnt[PER], fl[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    X[j] = Z[j] = 0;
+    cnt[j] = 0;
+    fl[j] = 0;
+    if (k0 + j < T) {
+      const SegInfo& si = a.seg_info[k0 + j];
+      X[j] = si.X;
+      Z[j] = si.Z;
+      cnt[j] = si.cnt;
+      fl[j] = si.flags;
+    }
+  }
+  const bool last_wg = blockIdx.x == gridDim.x - 1;
+  if (skip) {  // what fixup_kernel publishes when the piece was not walked
+    if (last_wg && tid == 0) {
+      st->active = 0;
+      st->piece_cuts = 0;
+      if (*a.pc.overflow) st->err |= kErrDense;
+      publish(a, st);
+    }
+    return;
+  }
+  s_lx[tid] = X[PER - 1];
+  s_lz[tid] = Z[PER - 1];
+  s_lf[tid] = fl[PER - 1];
+  if (tid == 0) s_last_seg = -1;
+  __syncthreads();
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t k = k0 + j;
+    if (k >= T) break;
+    bad = bad || (fl[j] & kBad) != 0;
+    if (k > 0) {
+      const uint64_t px = j ? X[j - 1] : s_lx[tid - 1];
+      const uint64_t pz = j ? Z[j - 1] : s_lz[tid - 1];
+      const uint32_t pf = j ? fl[j - 1] : s_lf[tid - 1];
+      bad = bad || px != pz || (pf & kBad) != 0;
+    }
+  }
+  if (__syncthreads_or(bad)) {  // a suspect segment: workgroup 0 does it all
+    if (blockIdx.x != 0) return;
+    fixup_body<NT>(a);
+    __threadfence_block();
+    __syncthreads();
+    if (!st->active || (st->err & kErrCapacity)) return;
+    for (uint32_t k = tid; k < T; k += NT) {
+      const uint32_t scnt = (a.seg_info[k].flags & kBad) ? 0u : a.seg_info[k].cnt;
+      const uint32_t rc = a.rep_cnt[k], rf = a.rep_from[k];
+      const uint64_t off = a.out_off[k];
+      const uint64_t* rep = a.rep + (uint64_t)k * a.scap;
+      const uint64_t* stg = a.stage + (uint64_t)k * a.scap;
+      for (uint32_t i = 0; i < rc; ++i) a.out[off + i] = rep[i];
+      for (uint32_t i = rf; i < scnt; ++i) a.out[off + rc + (i - rf)] = stg[i];
+    }
+    return;
+  }
+  // every staged list is the true chain: counts -> offsets
+  uint64_t mine = 0, my_last = 0;
+  int last_nonempty = -1;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    mine += cnt[j];
+    if (cnt[j]) {
+      last_nonempty = (int)(k0 + j);
+      my_last = Z[j];
+    }
+  }
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  uint64_t incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t v = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  if (lane == 63) s_part[wv] = incl;
+  atomicMax(&s_last_seg, last_nonempty);
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t acc = 0;
+    for (int i = 0; i < NT / 64; ++i) {
+      const uint64_t v = s_part[i];
+      s_part[i] = acc;
+      acc += v;
+    }
+    s_piece = acc;
+  }
+  __syncthreads();
+  {
+    uint64_t off = base + s_part[wv] + (incl - mine);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (k0 + j < T) {
+        s_off[k0 + j] = off;
+        s_cnt[k0 + j] = cnt[j];
+      }
+      off += cnt[j];
+    }
+  }
+  if (last_nonempty >= 0 && last_nonempty == s_last_seg) s_carry = my_last;
+  __syncthreads();
+  const uint64_t piece = s_piece;
+  const bool fits = base + piece <= a.out_cap;
+  if (fits) {
+    // this workgroup's segments, wave wv takes kb + wv + 4q: the loads of
+    // its segments are issued together (one memory round trip)
+    constexpr int QW = (int)kFinSegPerWg / (NT / 64);
+    const uint32_t kb = blockIdx.x * kFinSegPerWg;
+    const uint32_t ke = kb + kFinSegPerWg < T ? kb + kFinSegPerWg : T;
+    const uint32_t sc1 = a.scap - 1;
+    uint64_t v[QW];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      uint32_t k = kb + wv + (uint32_t)q * (NT / 64);
+      k = k < T ? k : T - 1;
+      v[q] = a.stage[(uint64_t)k * a.scap + (lane < sc1 ? lane : sc1)];
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const uint32_t k = kb + wv + (uint32_t)q * (NT / 64);
+      if (k < ke && lane < s_cnt[k]) a.out[s_off[k] + lane] = v[q];
+    }
+#pragma unroll 1
+    for (int q = 0; q < QW; ++q) {  // lists of more than 64 cuts
+      const uint32_t k = kb + wv + (uint32_t)q * (NT / 64);
+      if (k >= ke) break;
+      for (uint32_t i = 64 + lane; i < s_cnt[k]; i += 64)
+        a.out[s_off[k] + i] = a.stage[(uint64_t)k * a.scap + i];
+    }
+  }
+  if (last_wg && tid == 0) {
+    if (s_last_seg >= 0) st->carry = s_carry;
+    if (a.chain.is_last && st->carry >= a.chain.L) st->done = 1;
+    st->piece_cuts = piece;
+    if (!fits) st->err |= kErrCapacity;
+    st->total = base + piece;
+    st->active = 1;
+    publish(a, st);
+  }
+}
+template __global__ void finish_kernel<1>(StitchArgs);
+template __global__ void finish_kernel<2>(StitchArgs);
+template __global__ void finish_kernel<4>(StitchArgs);
+template __global__ void finish_kernel<8>(StitchArgs);
 
 // The chain state of a stitch-only pass (a shard re-walked from its true
 // entry over kept candidate lists; normally the scan initialises it).
