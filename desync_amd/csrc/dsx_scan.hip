@@ -865,10 +865,17 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         for (int q = 1; q < 8; ++q) mn = __builtin_elementwise_min(mn, t[q]);
         if (__builtin_expect(__ballot(mn < thr) != 0, 0)) {
           uint32_t bits = 0;
+          if (MODE == 2 && tcv.rot == 0) {
+            // odd d (k = 0, the default parameters): t = (h+1)*inv here, and
+            // chunker.go:265's test is t - qBias <= qMax with no rotate
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            if constexpr (MODE == 2) bits |= (mode2_exact(t[q] - 1u, tcv) ? 1u : 0u) << q;
-            else bits |= (t[q] == 0u ? 1u : 0u) << q;
+            for (int q = 0; q < 8; ++q) bits |= (t[q] - tcv.qbias <= tcv.qmax ? 1u : 0u) << q;
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              if constexpr (MODE == 2) bits |= (mode2_exact(t[q] - 1u, tcv) ? 1u : 0u) << q;
+              else bits |= (t[q] == 0u ? 1u : 0u) << q;
+            }
           }
           if (bits) {
             const uint32_t e = (bits << 16) | (o0 + (uint32_t)(g * 8));
