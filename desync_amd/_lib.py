@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("DSX_LIB_PATH") or os.path.join(HERE, "libdsx.so")  # 
 DSX_OUT_HOST = 0
 DSX_OUT_DEVICE = 1
 DSX_NO_SYNC = 2
+DSX_TIMED = 16
 DSX_SEAM_MAX_CANDS = 1024
 DSX_SEAM_MAX_CUTS = 1024
 

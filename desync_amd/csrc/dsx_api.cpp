@@ -233,6 +233,8 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   for (uint32_t i = 0; i < kQueueDepth; ++i)
     if (c->q_ev[i]) (void)hipEventDestroy(c->q_ev[i]);
   for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
+  for (auto& v : c->q_pev)
+    for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   delete c;
@@ -693,8 +695,16 @@ extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
   }
   c->stats.chunks = s.total;
   c->stats.repaired_segments = s.repaired;
-  c->stats.scan_ms = 0;  // queued calls are not timed (no events between their kernels)
-  c->stats.stitch_ms = 0;
+  float scan = 0, stitch = 0;  // untimed queued calls record no events
+  for (uint32_t i = 0; i < q.npiece; ++i) {
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, c->q_pev[q.slot][3 * i], c->q_pev[q.slot][3 * i + 1]);
+    (void)hipEventElapsedTime(&b, c->q_pev[q.slot][3 * i + 1], c->q_pev[q.slot][3 * i + 2]);
+    scan += a;
+    stitch += b;
+  }
+  c->stats.scan_ms = scan;
+  c->stats.stitch_ms = stitch;
   *n_out = s.total;
   if ((s.err & kErrCapacity) || s.total > q.cap) return DSX_E_CAPACITY;
   return DSX_OK;
@@ -725,10 +735,15 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
     q.slot = c->q_next++ % kQueueDepth;
     q.done = c->q_ev[q.slot];
     c->h_cur = &c->h_ring[q.slot];
-    // queued calls record no timing events: an event record between two
-    // kernels of a stream costs ~6 us of GPU time (rocprofv3 kernel trace)
-    c->timing = false;
+    // queued calls record no timing events unless DSX_TIMED: an event record
+    // between two kernels of a stream costs ~6 us of GPU time (rocprofv3
+    // kernel trace).  A timed call records into its slot's own events.
+    const bool timed = (flags & DSX_TIMED) != 0;
+    c->timing = timed;
+    if (timed) std::swap(c->pev, c->q_pev[q.slot]);
     rc = run_device(c, (const uint8_t*)d_blob, len, cc);
+    if (timed) std::swap(c->pev, c->q_pev[q.slot]);
+    q.npiece = timed ? c->npiece_call : 0u;
     c->timing = true;
     c->h_cur = c->h_state;
     if (rc) return rc;

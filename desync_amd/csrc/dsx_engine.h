@@ -212,7 +212,9 @@ struct dsx_ctx {
     uint32_t slot = 0;
     uint64_t seq = 0;       // piece sequence number of the call's last piece
     hipEvent_t done = nullptr;
+    uint32_t npiece = 0;    // DSX_TIMED: pieces whose events are in q_pev[slot]
   };
+  std::vector<hipEvent_t> q_pev[kQueueDepth];  // DSX_TIMED queued calls' piece events
   std::deque<Pending> pend;
   HostState* h_ring = nullptr;   // pinned, kQueueDepth slots
   HostState* h_cur = nullptr;    // slot the next enqueued piece publishes into

@@ -98,6 +98,9 @@ int dsx_cancel(dsx_ctx_t *ctx);
 #define DSX_NO_SYNC 2u    /* (device output only) enqueue on the ctx stream and return;
                              up to 8 such calls may be queued (they run in order);
                              dsx_result() waits for the OLDEST and returns its count */
+#define DSX_TIMED 16u     /* with DSX_NO_SYNC: record the call's scan/stitch events
+                             (dsx_get_stats after its dsx_result reports them); untimed
+                             queued calls record none (an event costs ~6 us of stream time) */
 
 /* Device-resident blob (HBM) -> cut list.  d_blob must stay valid until the
  * call (or, with DSX_NO_SYNC, dsx_sync()) returns.  If cap is too small the

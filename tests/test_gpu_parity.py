@@ -656,13 +656,19 @@ def test_queued_no_sync_calls(dctx):
         refs.append(o.chunk_stream(arr, MIN, AVG, MAX))
         outs.append(torch.empty(arr.size // MIN + 4, dtype=torch.int64, device="cuda"))
     cnt = ctypes.c_uint64()
-    for t, out in zip(blobs, outs):
+    for i, (t, out) in enumerate(zip(blobs, outs)):
+        timed = _lib.DSX_TIMED if i % 2 else 0  # odd calls record their events
         _lib.check(L.dsx_cut_device(dctx.h, ctypes.c_void_p(t.data_ptr()), t.numel(),
                                     ctypes.byref(p.c), ctypes.c_void_p(out.data_ptr()),
                                     out.numel(), ctypes.byref(cnt),
-                                    _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC), dctx.h)
-    for ref, out in zip(refs, outs):
+                                    _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC | timed), dctx.h)
+    for i, (ref, out) in enumerate(zip(refs, outs)):
         _lib.check(L.dsx_result(dctx.h, ctypes.byref(cnt)), dctx.h)
         assert cnt.value == ref.size
         assert np.array_equal(out[:cnt.value].cpu().numpy().astype(np.uint64), ref)
+        st = dctx.stats()
+        if i % 2:  # DSX_TIMED: the call's own scan and stitch times
+            assert 0 < st.scan_ms < 100 and 0 < st.stitch_ms < 100
+        else:
+            assert st.scan_ms == 0 and st.stitch_ms == 0
     assert L.dsx_result(dctx.h, ctypes.byref(cnt)) == _lib.DSX_E_STATE
