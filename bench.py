@@ -215,37 +215,31 @@ def main():
         shard = lanes[0]
 
     # N = 1: every step is one complete dsx_cut_device job (scan + stitch, cut
-    # list in HBM) whose count the host collects.  Jobs rotate over `inflight`
-    # contexts (own stream and scratch each): job s is enqueued before the
-    # host waits for job s-1, so the GPU is not idle while the host wakes up.
-    nctx = max(1, args.inflight) if world == 1 else 1
-    ctxs = [ctx] + [_lib.Context(gpu) for _ in range(nctx - 1)]
-    outs = [out] + [torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(nctx - 1)]
-    pending = [False] * nctx
+    # list in HBM) whose count the host collects.  Up to `inflight` jobs are
+    # queued on the context (DSX_NO_SYNC): job s is enqueued before the host
+    # waits for job s - inflight, so the GPU is not idle while the host wakes
+    # up, and the library runs job s's stitch beside job s+1's scan (its scans
+    # own a CU-masked stream).
+    depth = min(8, max(1, args.inflight)) if world == 1 else 1
+    outs = [torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(depth)]
+    queued = []
     scan_ms = []
     stitch_ms = []
     cnt = ctypes.c_uint64()
 
-    def collect(i, record):
-        c = ctxs[i]
-        _lib.check(L.dsx_result(c.h, ctypes.byref(cnt)), c.h)
-        pending[i] = False
-        if record:
-            st = c.stats()
-            scan_ms.append(st.scan_ms)
-            stitch_ms.append(st.stitch_ms)
+    def collect():
+        _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
+        queued.pop(0)
         return cnt.value
 
     def step(s, record=False):
         if world == 1:
-            i = s % nctx
-            got = collect(i, record) if pending[i] else None
-            c = ctxs[i]
-            _lib.check(L.dsx_cut_device(c.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
-                                        ctypes.c_void_p(outs[i].data_ptr()), cap,
+            got = collect() if len(queued) == depth else None
+            _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
+                                        ctypes.c_void_p(outs[s % depth].data_ptr()), cap,
                                         ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
-                       c.h)
-            pending[i] = True
+                       ctx.h)
+            queued.append(s)
             return got
         # N > 1: chunk this rank's shard, RCCL all-gather of the 16 KiB seam
         # records in HBM, resolve the seams (desync_amd/shard.py)
@@ -253,10 +247,8 @@ def main():
 
     def drain(nsteps, record):
         last = None
-        for j in range(nctx):
-            i = (nsteps + j) % nctx  # oldest job first
-            if pending[i]:
-                last = collect(i, record)
+        while queued:
+            last = collect()
         return last
 
     def run_lanes(nsteps):
@@ -396,7 +388,7 @@ def main():
                 "bytes_per_gpu": n,
                 "chunks": int(chunks),
                 "parallelism": f"range-shard x{world}" if world > 1 else "single GPU",
-                "jobs_in_flight": nctx if world == 1 else len(lanes),
+                "jobs_in_flight": depth if world == 1 else len(lanes),
             },
         }
         if world == 1 and scan_ms:
@@ -420,8 +412,7 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
-    for c in ctxs:
-        c.close()
+    ctx.close()
 
 
 if __name__ == "__main__":

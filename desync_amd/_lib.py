@@ -55,7 +55,7 @@ EXPORTS = (
     "dsx_stream_pop_many", "dsx_stream_window", "dsx_stream_unpop", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host", "dsx_copy",
-    "dsx_ids_fd", "dsx_ids_host",
+    "dsx_ids_fd", "dsx_ids_host", "dsx_progress",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -141,6 +141,7 @@ def lib():
             "dsx_ctx_destroy": (i32, [vp]),
             "dsx_last_error": (ctypes.c_char_p, [vp]),
             "dsx_cancel": (i32, [vp]),
+            "dsx_progress": (i32, [vp, P(u64)]),
             "dsx_cut_device": (i32, [vp, vp, u64, P(Params), vp, u64, P(u64), u32]),
             "dsx_sync": (i32, [vp]),
             "dsx_result": (i32, [vp, P(u64)]),
@@ -264,3 +265,13 @@ class pooled_context:
             _pool.setdefault(self.device, []).append(self.ctx)
         self.ctx = None
         return False
+
+
+def reset_context_pool():
+    """Closes the idle pooled contexts (settings such as DSX_INDEX_WINDOW are
+    read from the environment when a context is created)."""
+    with _lock:
+        idle = [c for cs in _pool.values() for c in cs]
+        _pool.clear()
+    for c in idle:
+        c.close()

@@ -74,8 +74,14 @@ class Chunker:
     """Content-defined chunker over a file-like reader (``readinto(buf)`` or
     ``read(n)``)."""
 
-    def __init__(self, reader, min_size, avg_size, max_size, ctx=None, device=0):
+    def __init__(self, reader, min_size, avg_size, max_size, ctx=None, device=0, zero_copy=False):
         self.params = Params(min_size, avg_size, max_size)
+        # Next()'s chunk: a bytes copy by default.  zero_copy=True hands out a
+        # read-only view of the library's pinned buffer instead (Go's aliasing
+        # rule, chunker.go:202-205: valid until the next call on this
+        # Chunker), which a caller must not keep: the library may move or free
+        # that buffer, and a stale view is a dangling pointer, not stale data.
+        self._zero_copy = bool(zero_copy)
         self.r = reader
         # Like a Go Chunker (its own buffer and hash state, chunker.go:108-131)
         # every Chunker owns a library context: the stream state and device
@@ -108,7 +114,8 @@ class Chunker:
 
     # -- reference API -----------------------------------------------------
     def Next(self):
-        """(start, chunk view); (start, empty) when the stream is exhausted."""
+        """(start, chunk bytes); (start, empty) when the stream is exhausted.
+        With zero_copy the chunk is a view valid until the next call."""
         L = lib()
         h = self.ctx.h
         mx = self.params.max
@@ -132,7 +139,7 @@ class Chunker:
                 self._win = None
                 return self._take()
             if self._eof:
-                return self._start.value, memoryview(b"")
+                return self._start.value, (memoryview(b"") if self._zero_copy else b"")
             if self._err is not None:
                 if self._synced:  # cannot happen: the next chunk ends before _E
                     raise RuntimeError("stream stalled behind a reader error")
@@ -154,7 +161,8 @@ class Chunker:
         self._cur = e
         if self._idbuf is not None:
             self._last_id = self._qids[32 * i:32 * i + 32]
-        return s, self._win[s - self._wbase:e - self._wbase]
+        v = self._win[s - self._wbase:e - self._wbase]
+        return s, (v if self._zero_copy else v.tobytes())
 
     def EnableIDs(self, algo=None):
         """Compute every chunk's Digest.Sum on the GPU next to its cut (for

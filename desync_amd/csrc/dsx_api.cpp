@@ -194,8 +194,22 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     const long lb = atol(v);
     if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
   }
+  if (const char* v = getenv("DSX_STITCH_CUS")) c->stitch_cus = std::max(0, std::min(c->ncu / 2, atoi(v)));
   CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  c->scan_stream = c->stream;
+  if (c->stitch_cus > 0) {
+    // the scans' CU mask leaves the last stitch_cus CUs to the stitch kernels
+    std::vector<uint32_t> mask((c->ncu + 31) / 32, 0u);
+    for (int i = 0; i < c->ncu - c->stitch_cus; ++i) mask[i / 32] |= 1u << (i % 32);
+    hipStream_t ss = nullptr;
+    CREATE_STEP(hipExtStreamCreateWithCUMask(&ss, (uint32_t)mask.size(), mask.data()));
+    c->scan_stream = ss;
+    for (int i = 0; i < 2; ++i) {
+      CREATE_STEP(hipEventCreateWithFlags(&c->ev_scan[i], hipEventDisableTiming));
+      CREATE_STEP(hipEventCreateWithFlags(&c->ev_stitch[i], hipEventDisableTiming));
+    }
+  }
   CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
   CREATE_STEP(hipHostMalloc((void**)&c->h_ring, kQueueDepth * sizeof(HostState)));
   memset(c->h_ring, 0, kQueueDepth * sizeof(HostState));
@@ -205,8 +219,10 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   CREATE_STEP(hipHostMalloc((void**)&c->h_res, 4 * sizeof(uint64_t)));
   memset(c->h_state, 0, sizeof(HostState));
   CREATE_STEP(c->state.ensure(1));
-  CREATE_STEP(c->overflow.ensure(4));  // [0..1] overflow, [2..3] scan work queue (parity)
-  CREATE_STEP(hipMemset(c->overflow.p, 0, 4 * sizeof(uint32_t)));
+  // [0..1] overflow (piece parity); [32 + 256*parity + 32*x] the scan's work
+  // queue counter x = 0..7 (one per XCD, each on its own 128-B line)
+  CREATE_STEP(c->overflow.ensure(kQueueWords));
+  CREATE_STEP(hipMemset(c->overflow.p, 0, kQueueWords * sizeof(uint32_t)));
   CREATE_STEP(hipMemset(c->state.p, 0, sizeof(DevState)));
 #undef CREATE_STEP
   *out = c;
@@ -218,7 +234,9 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  if (c->scan_stream && c->scan_stream != c->stream) (void)hipStreamSynchronize(c->scan_stream);
   c->region_cnt.release(); c->region_list.release(); c->overflow.release(); c->rep_cnt.release(); c->rep_from.release();
+  c->region_cnt2.release(); c->region_list2.release();
   c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
   c->dg_ends.release(); c->dg_ids.release(); c->dg_queue.release();
   c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
@@ -235,6 +253,11 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
   for (auto& v : c->q_pev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i) {
+    if (c->ev_scan[i]) (void)hipEventDestroy(c->ev_scan[i]);
+    if (c->ev_stitch[i]) (void)hipEventDestroy(c->ev_stitch[i]);
+  }
+  if (c->scan_stream && c->scan_stream != c->stream) (void)hipStreamDestroy(c->scan_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   delete c;
@@ -249,12 +272,33 @@ extern "C" int dsx_cancel(dsx_ctx_t* c) {
   return DSX_OK;
 }
 
+// pb.Set(chunk.Start + chunk.Size) per assembled chunk (make.go:134-140): the
+// end of the last confirmed chunk of the running (or last) index / cut call.
+// Each piece's last stitch kernel publishes the chain position into pinned
+// host memory; this reads it without touching the context's streams, so a
+// second thread may call it while the call runs.  Monotone within a call.
+extern "C" int dsx_progress(dsx_ctx_t* c, uint64_t* bytes) {
+  if (!c || !bytes) return DSX_E_INVAL;
+  uint64_t v = c->prog_done.load();
+  if (c->prog_active.load()) {
+    const uint64_t cur = ((volatile HostState*)c->h_state)->carry;
+    if (cur > v && cur <= c->prog_len.load()) {
+      uint64_t seen = v;
+      while (seen < cur && !c->prog_done.compare_exchange_weak(seen, cur)) {
+      }
+      v = seen > cur ? seen : cur;
+    }
+  }
+  *bytes = v;
+  return DSX_OK;
+}
+
 extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64_t* n_scan,
                                uint64_t* n_walk) {
   if (!c || !n_scan || !n_walk) return DSX_E_INVAL;
   *n_scan = c->trace_n;
   *n_walk = c->trace_walk_n;
-  const uint64_t words = 3 * c->trace_n + 10 * c->trace_walk_n;
+  const uint64_t words = 4 * c->trace_n + 10 * c->trace_walk_n;
   if (!words || !out) return DSX_OK;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -319,7 +363,9 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   const bool line = c->scan_line && !cc.dense && P >= delta;
   const int W = line ? c->scanl_waves : kCfgWaves[c->scan_cfg];
   const int cfgBR = kCfgBR[c->scan_cfg];
-  const uint64_t slots_total = (uint64_t)c->ncu * W;  // wave slots
+  const bool split = c->scan_stream != c->stream;
+  const int ncu_scan = c->ncu - (split ? c->stitch_cus : 0);  // CUs of the scan's mask
+  const uint64_t slots_total = (uint64_t)ncu_scan * W;         // wave slots
   const uint64_t span = line ? len + delta : len;       // grid bytes
   uint32_t S, LS;
   uint32_t batches;
@@ -336,7 +382,10 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     // lane segments longer than the target lose HBM efficiency (lane stride
     // 33 KB: 4.85 TB/s staging vs 6.24 TB/s at 8448 B, tools/ubench_staging.hip);
     // bigger pieces take more regions per wave slot from the work queue
-    m = std::min<uint64_t>(m, c->lane_target / (3 * kLine));
+    // (up to two trips past the target when that keeps every region in the
+    // first pass: a second pass for a few regions costs a whole region time)
+    const uint64_t mcap = c->lane_target / (3 * kLine);
+    if (m > mcap + 2 || rounds_needed > 1) m = std::min<uint64_t>(m, mcap);
     m = std::max<uint64_t>(1, std::min<uint64_t>(m, kLineLaneMax / (3 * kLine)));
     S = (uint32_t)(3 * kLine * m);
     if (c->lane_bytes_override && c->lane_bytes_override % (3 * kLine) == 0 &&
@@ -389,12 +438,21 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     rcnt = kp->cnt.p;
     rlist = kp->list.p;
   } else {
-    HIPCHK(c, grow(c, c->region_cnt, nregions));
-    HIPCHK(c, grow(c, c->region_list, nregions * rcap));
-    rcnt = c->region_cnt.p;
-    rlist = c->region_list.p;
+    // split streams: two region-list sets, so the next piece's scan writes
+    // one while this piece's stitch reads the other
+    const bool second = split && (c->piece_seq + 1) % 2 == 1;
+    auto& bc = second ? c->region_cnt2 : c->region_cnt;
+    auto& bl = second ? c->region_list2 : c->region_list;
+    HIPCHK(c, grow(c, bc, nregions));
+    HIPCHK(c, grow(c, bl, nregions * rcap));
+    rcnt = bc.p;
+    rlist = bl.p;
   }
+  c->last_rcnt = rcnt;
+  c->last_rlist = rlist;
   const uint64_t seq = ++c->piece_seq;
+  const int par = (int)(seq & 1);
+  hipStream_t ss = c->scan_stream;
 
   ScanArgs sa{};
   sa.base = d_piece;
@@ -412,13 +470,13 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.lane_slot = c->lane_slot.p;
   sa.region_cnt = rcnt;
   sa.region_list = rlist;
-  sa.overflow = c->overflow.p + (seq & 1);
-  sa.overflow_next = c->overflow.p + ((seq + 1) & 1);
-  sa.queue = c->overflow.p + 2 + (seq & 1);
-  sa.queue_next = c->overflow.p + 2 + ((seq + 1) & 1);
-  sa.state_init = c->init_pending ? (void*)c->state.p : nullptr;
+  // overflow word and queue counters: slot seq % 4; the scan zeroes the next
+  // piece's slot (the stitch of the previous piece may still read its own)
+  sa.overflow = c->overflow.p + (seq % kQueueSlots);
+  sa.overflow_next = c->overflow.p + ((seq + 1) % kQueueSlots);
+  sa.queue = c->overflow.p + 32 + 256 * (seq % kQueueSlots);
+  sa.queue_next = c->overflow.p + 32 + 256 * ((seq + 1) % kQueueSlots);
   sa.wave_major = c->wave_major ? 1u : 0u;
-  sa.init_carry = c->init_carry;
   if (line) {
     // region 0's descriptor: the warm-up line unless it would start before
     // the readable bytes (then the 16-B step at or below base - min(halo, 48))
@@ -431,28 +489,29 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   c->last_grid_P = line ? P - delta : P;
   if (c->scan_trace && line) {
     c->trace_n = (uint64_t)c->ncu * W;
-    HIPCHK(c, grow(c, c->trace, 3 * c->trace_n + 10 * 65536));
-    HIPCHK(c, hipMemsetAsync(c->trace.p, 0, 3 * c->trace_n * sizeof(uint64_t), c->stream));
+    HIPCHK(c, grow(c, c->trace, 4 * c->trace_n + 10 * 65536));
+    HIPCHK(c, hipMemsetAsync(c->trace.p, 0, 4 * c->trace_n * sizeof(uint64_t), ss));
     sa.trace = c->trace.p;
   }
-  c->init_pending = false;
   const uint32_t pi = c->npiece_call++;
   while (c->pev.size() < 3 * (size_t)(pi + 1)) {
     hipEvent_t e;
     HIPCHK(c, hipEventCreate(&e));
     c->pev.push_back(e);
   }
-  if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi], c->stream));
+  // the region lists this scan writes were read by the stitch two pieces ago
+  if (split) HIPCHK(c, hipStreamWaitEvent(ss, c->ev_stitch[par], 0));
+  if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi], ss));
   {
     const uint64_t need_wg = std::max<uint64_t>(1, (nregions + W - 1) / W);
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)c->ncu);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)ncu_scan);
     const dim3 g(grid), b(W * kWave);
     const int mode = pick_mode(c, p->discriminator);
 #if DSX_DIAG
 #define DSX_ABLATE(K, ...)                                                                 \
-  if (c->variant == 1) hipLaunchKernelGGL((K<2, 1, __VA_ARGS__>), g, b, 0, c->stream, sa); \
-  else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__>), g, b, 0, c->stream, sa); \
-  else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__>), g, b, 0, c->stream, sa); \
+  if (c->variant == 1) hipLaunchKernelGGL((K<2, 1, __VA_ARGS__>), g, b, 0, ss, sa); \
+  else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__>), g, b, 0, ss, sa); \
+  else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__>), g, b, 0, ss, sa); \
   else
 #else
 #define DSX_ABLATE(K, ...)
@@ -461,17 +520,17 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   do {                                                                                     \
     DSX_ABLATE(scan_kernel, BR, NB, WV, SUB, PF)                                           \
     if (mode == 2)                                                                         \
-      hipLaunchKernelGGL((scan_kernel<2, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+      hipLaunchKernelGGL((scan_kernel<2, 0, BR, NB, WV, SUB, PF>), g, b, 0, ss, sa); \
     else if (mode == 1)                                                                    \
-      hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+      hipLaunchKernelGGL((scan_kernel<1, 0, BR, NB, WV, SUB, PF>), g, b, 0, ss, sa); \
     else                                                                                   \
-      hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB, PF>), g, b, 0, c->stream, sa); \
+      hipLaunchKernelGGL((scan_kernel<0, 0, BR, NB, WV, SUB, PF>), g, b, 0, ss, sa); \
   } while (0)
 #if DSX_DIAG
 #define DSX_TRACE_VARIANTS(WV, SUB, D)                                                    \
-  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D>), g, b, 0, c->stream, sa); \
+  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D>), g, b, 0, ss, sa); \
   else if (c->variant == 6 && mode == 2)                                                  \
-    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D>), g, b, 0, c->stream, sa);         \
+    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D>), g, b, 0, ss, sa);         \
   else
 #else
 #define DSX_TRACE_VARIANTS(WV, SUB, D)
@@ -481,11 +540,11 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     DSX_ABLATE(scanl_kernel, WV, SUB, D)                                                  \
     DSX_TRACE_VARIANTS(WV, SUB, D)                                                        \
     if (mode == 2)                                                                        \
-      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
+      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D>), g, b, 0, ss, sa);       \
     else if (mode == 1)                                                                   \
-      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
+      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D>), g, b, 0, ss, sa);       \
     else                                                                                  \
-      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D>), g, b, 0, c->stream, sa);       \
+      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D>), g, b, 0, ss, sa);       \
   } while (0)
     if (line) {
       DSX_LAUNCHL(8, 8, 1);
@@ -512,7 +571,11 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
 #undef DSX_TRACE_VARIANTS
     HIPCHK(c, hipGetLastError());
   }
-  if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], c->stream));
+  if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi + 1], ss));
+  if (split) {  // the stitch (ctx stream) after the scan (scan stream)
+    HIPCHK(c, hipEventRecord(c->ev_scan[par], ss));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scan[par], 0));
+  }
   PieceCands pc{};
   pc.P = c->last_grid_P;  // region r covers (P' + r*RB, P' + (r+1)*RB]
   pc.RB = region_bytes;
@@ -528,6 +591,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   }
   int rc = launch_stitch(c, cc, pc, P, len, is_last, seq, line && c->scan_trace);
   if (rc) return rc;
+  if (split) HIPCHK(c, hipEventRecord(c->ev_stitch[par], c->stream));
   if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi + 2], c->stream));
   c->stats.pieces++;
   return DSX_OK;
@@ -583,9 +647,12 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   ta.state = c->state.p;
   ta.host_state = c->h_cur;
   ta.seq = seq;
+  ta.init = c->init_pending ? 1u : 0u;  // the call's first piece: walk_kernel resets the state
+  ta.init_carry = c->init_carry;
+  c->init_pending = false;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
   if (trace && walk_grid <= 65536) {
-    ta.trace = c->trace.p + 3 * c->trace_n;
+    ta.trace = c->trace.p + 4 * c->trace_n;
     c->trace_walk_n = walk_grid;
   }
   const size_t walk_lds = (size_t)kWalkLdsCap * 4 + (kMaxSpg + 1) * 8;
@@ -1016,8 +1083,8 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
           pc.RB = c->last_region_bytes;
           pc.nregions = c->last_nregions;
           pc.region_cap = c->last_region_cap;
-          pc.region_cnt = cc.keep ? sh.kept[0].cnt.p : c->region_cnt.p;
-          pc.region_list = cc.keep ? sh.kept[0].list.p : c->region_list.p;
+          pc.region_cnt = cc.keep ? sh.kept[0].cnt.p : c->last_rcnt;
+          pc.region_list = cc.keep ? sh.kept[0].list.p : c->last_rlist;
           pc.overflow = nullptr;
           hipLaunchKernelGGL(seam_cands_kernel, dim3(1), dim3(64), 0, c->stream, pc, sh.start,
                              wend0, c->d_seam.p);

@@ -61,10 +61,9 @@ struct ScanArgs {
   uint32_t* region_list; // [nregions*region_cap] sorted offsets in (0, 64*S] from region base
   uint32_t* overflow;    // regions whose lanes or list overflowed (-> dense path)
   uint32_t* overflow_next;  // the next piece's counter: zeroed here (parity buffers)
-  uint32_t* queue;       // region work queue (regions beyond the first wave slot pass)
-  uint32_t* queue_next;  // the next piece's queue counter: zeroed here
-  void* state_init;      // if non-null: DevState to initialise (first piece of a call)
-  uint64_t init_carry;
+  uint32_t* queue;       // region work queue (regions beyond the first wave slot pass):
+                         // 8 counters (one per XCD) at queue[32*x]
+  uint32_t* queue_next;  // the next piece's queue counters: zeroed here
   // line-aligned scan (scanl_kernel): the lane grid starts at base - delta,
   // the 128-B line holding base[0]; region 0's descriptor starts shift0 bytes
   // into its warm-up line (bytes before it read as zeros)
@@ -78,6 +77,8 @@ struct ScanArgs {
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches
 // of one 128-B line per lane, so the ring phase repeats), offsets in u16
 constexpr int kLine = 128;
+constexpr int kQueueSlots = 4;                  // overflow / queue slots (piece seq mod 4)
+constexpr int kQueueWords = 32 + kQueueSlots * 256;  // overflow words + 4 x 8 queue counters
 constexpr uint32_t kLineLaneMax = 384u * 170u;  // 65280
 
 // Sentinel for "successor depends on bytes beyond the piece" (non-final piece).

@@ -94,8 +94,20 @@ struct dsx_ctx {
   int device = 0;
   int ncu = 256;
   hipStream_t stream = nullptr, copy_stream = nullptr;
+  // Scans run on scan_stream, CU-masked to all but `stitch_cus` CUs, and
+  // everything else (the stitch, digests, copies, host syncs) on `stream`: a
+  // piece's stitch then overlaps the next piece's scan on the CUs the scan
+  // leaves free.  stitch_cus == 0: scan_stream == stream.
+  hipStream_t scan_stream = nullptr;
+  int stitch_cus = 8;                      // DSX_STITCH_CUS
+  hipEvent_t ev_scan[2] = {}, ev_stitch[2] = {};  // per region-list set (piece parity)
   bool timing = true;  // record the per-piece scan/stitch events (stats.scan_ms/stitch_ms)
   std::atomic<int> cancel{0};
+  // dsx_progress (another thread may read it while an index/cut call runs):
+  // bytes up to the last confirmed cut of the running or last call
+  std::atomic<uint64_t> prog_done{0};
+  std::atomic<uint64_t> prog_len{0};
+  std::atomic<int> prog_active{0};  // the running call's pieces publish into h_state
   std::string err;
   int force_mode = -1;  // DSX_TEST_MODE env override
   int variant = 0;      // DSX_SCAN_VARIANT: diagnostic scan ablations (wrong results)
@@ -114,11 +126,14 @@ struct dsx_ctx {
   bool wave_major = true;             // DSX_WAVE_MAJOR: scanl's first regions wave-major
   bool finish = true;                 // DSX_FINISH=0: fixup_fast_kernel + gather_kernel instead of finish_kernel
   bool fixup_fast = true;             // DSX_FIXUP_FAST=0: fixup_kernel for every piece
-  DevBuf<uint64_t> trace;       // [3 * trace_n scan records][10 * trace_walk_n walk records]
+  DevBuf<uint64_t> trace;       // [4 * trace_n scan records][10 * trace_walk_n walk records]
   uint64_t trace_n = 0, trace_walk_n = 0;
   uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;
+  DevBuf<uint32_t> region_cnt2, region_list2;  // the second region-list set (split streams)
+  const uint32_t* last_rcnt = nullptr;          // region lists of the last enqueued piece
+  const uint32_t* last_rlist = nullptr;
   DevBuf<uint32_t> lane_slot;
   DevBuf<SegInfo> seg_info;
   DevBuf<uint64_t> stage, rep, out_off, out;
@@ -243,8 +258,15 @@ inline hipError_t grow(dsx_ctx* c, DevBuf<T>& b, size_t n) {
   if (b.p) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->copy_stream);
+    if (c->scan_stream != c->stream) (void)hipStreamSynchronize(c->scan_stream);
   }
   return b.ensure(n + n / 4 + 64);
+}
+
+// The stream a piece's scan waits on for its input bytes (an H2D copy event,
+// dsx_index.cpp / dsx_stream.cpp): the scan stream.
+inline hipError_t scan_wait(dsx_ctx* c, hipEvent_t ev) {
+  return hipStreamWaitEvent(c->scan_stream, ev, 0);
 }
 
 int set_hip_err(dsx_ctx* c, hipError_t e, const char* what);

@@ -164,9 +164,24 @@ int index_setup(dsx_ctx* c, uint64_t slot_bytes) {
 int drain(dsx_ctx* c, Prefetcher& pf, int rc) {
   pf.stop();
   (void)hipStreamSynchronize(c->copy_stream);
+  (void)hipStreamSynchronize(c->scan_stream);
   (void)hipStreamSynchronize(c->stream);
   return rc;
 }
+
+// Marks the progress of a run_index call (dsx_progress) for its lifetime.
+struct ProgressScope {
+  dsx_ctx* c;
+  ProgressScope(dsx_ctx* cc, uint64_t len) : c(cc) {
+    c->prog_active.store(0);
+    c->prog_done.store(0);
+    c->prog_len.store(len);
+    ((volatile HostState*)c->h_state)->carry = 0;
+    c->prog_active.store(1);
+  }
+  ~ProgressScope() { c->prog_active.store(0); }
+  void set(uint64_t v) { c->prog_done.store(v); }
+};
 
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
               uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {
@@ -196,6 +211,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   if (algo >= 0) HIPCHK(c, grow(c, c->dg_ids, need * 32));
   const int K = dsx_ctx::kIdxSlots;
 
+  ProgressScope prog(c, len);
   for (int attempt = 0; attempt < 2; ++attempt) {
     CallCfg cc{p, len, 0, kRound, c->out.p, need, attempt == 1};
     rc = reset_state(c, 0);
@@ -203,8 +219,41 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     HIPCHK(c, hipMemsetAsync(c->idx_snap.p, 0, 2 * sizeof(uint64_t), c->stream));  // {0 cuts, cut 0}
     Prefetcher pf(fill, ud, len, piece, c->idx_slots, K, c->index_readers);
     uint64_t k = 0;  // piece index
-    for (uint64_t w = 0; w < nwin; ++w) {
-      const uint64_t ws = w * W, wl = std::min(W, len - ws);
+    uint64_t w = 0, ws = 0, wl = 0;
+    // Interrupted{} or a read error (make.go:133-162, :201-203): the chunks
+    // confirmed so far -- the chain up to the last stitched piece, a prefix
+    // of the true chain -- are returned with the error, IDs included: the
+    // current window's confirmed chunks are hashed first.
+    auto partial = [&](int err) -> int {
+      drain(c, pf, err);
+      if (algo >= 0) {
+        hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
+                           (const DevState*)c->state.p, c->idx_snap.p + 2 * (w + 1));
+        DigestArgs da{};
+        uint8_t* buf = c->idx_win[w & 1].p;
+        da.blob = w == 0 ? buf + pre : buf;
+        da.base_off = w == 0 ? 0 : ws - pre;
+        da.len = w == 0 ? wl : pre + wl;
+        da.ends = c->out.p;
+        da.ids = c->dg_ids.p;
+        da.range_lo = c->idx_snap.p + 2 * w;
+        da.range_hi = c->idx_snap.p + 2 * (w + 1);
+        if (launch_digest(c, da, (pre + wl) / p->min + 2, algo)) return err;
+      }
+      HostState st;
+      (void)hipStreamSynchronize(c->stream);
+      if (read_state(c, &st) || st.err) return err;  // (no piece stitched yet: nothing)
+      const uint64_t n = std::min<uint64_t>(st.total, cap);
+      if (n && hipMemcpy(out_ends, c->out.p, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return err;
+      if (n && out_ids && hipMemcpy(out_ids, c->dg_ids.p, n * 32, hipMemcpyDeviceToHost) != hipSuccess)
+        return err;
+      *n_out = n;
+      prog.set(n ? out_ends[n - 1] : 0);
+      return err;
+    };
+    for (w = 0; w < nwin; ++w) {
+      ws = w * W;
+      wl = std::min(W, len - ws);
       uint8_t* buf = c->idx_win[w & 1].p;
       // the digest of window w-2 read this buffer; the copy stream waits for it
       if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
@@ -213,11 +262,11 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
                                  hipMemcpyDeviceToDevice, c->copy_stream));
       uint64_t scanned = ws;
       for (uint64_t off = ws; off < ws + wl; off += piece, ++k) {
-        if (c->cancel.load()) return drain(c, pf, DSX_E_INTERRUPTED);
+        if (c->cancel.load()) return partial(DSX_E_INTERRUPTED);
         uint8_t* hp = nullptr;
         uint64_t hn = 0;
         rc = pf.wait(k, &hp, &hn);
-        if (rc) return drain(c, pf, rc);
+        if (rc) return partial(rc);
         hipError_t e = hipMemcpyAsync(buf + pre + (off - ws), hp, hn, hipMemcpyHostToDevice,
                                       c->copy_stream);
         if (e == hipSuccess) e = hipEventRecord(c->idx_copy_ev[k % K], c->copy_stream);
@@ -228,7 +277,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         if (k >= 1) pf.release(k - 1);
         const uint64_t end = off + hn;
         if (end == ws + wl || end - scanned >= scan_step) {
-          e = hipStreamWaitEvent(c->stream, c->idx_copy_ev[k % K], 0);
+          e = scan_wait(c, c->idx_copy_ev[k % K]);  // (the stitch follows the scan)
           if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: wait"));
           const uint64_t halo = w == 0 ? scanned : pre + (scanned - ws);
           c->timing = false;  // (no event records between the pipeline's kernels)
@@ -281,6 +330,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       HIPCHK(c, hipMemcpy(out_ends, c->out.p, st.total * 8, hipMemcpyDeviceToHost));
       if (out_ids) HIPCHK(c, hipMemcpy(out_ids, c->dg_ids.p, st.total * 32, hipMemcpyDeviceToHost));
     }
+    prog.set(len);
     return DSX_OK;
   }
   c->err = "dense-candidate path overflowed";

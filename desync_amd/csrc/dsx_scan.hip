@@ -324,19 +324,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   static_assert(LDSB <= kScanLds, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
 
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *a.overflow_next = 0u;  // parity buffers of the next piece (no reader now)
-    *a.queue_next = 0u;
-    if (a.state_init) {     // first piece of a call: reset the chain state
-      uint64_t* st = (uint64_t*)a.state_init;
-      st[0] = a.init_carry;  // DevState.carry
-      st[1] = 0;             // total
-      st[2] = 0;             // piece_cuts
-      st[3] = 0;             // repaired
-      st[4] = 0;             // done, err
-      st[5] = 0;             // active, pad
-    }
-  }
+  if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.overflow_next = 0u;  // (the next piece's slot)
   if constexpr (VARIANT == 4) {  // ablation: staging never filled -> zero bytes
     for (int e = threadIdx.x; e < W * NBUF * STG / 4; e += NT)
       reinterpret_cast<uint32_t*>(lds + kTableBytes)[e] = 0u;
@@ -624,20 +613,13 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   static_assert(LDSB <= kScanLds, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
   __shared__ uint32_t s_prog[kBal ? W : 1];  // batches hashed per wave (SIMD partner balancing)
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[256];  // the table, landed by LDS-DMA
+  // trace: the wave's first instruction (before the table fill)
+  const uint64_t t_entry = VARIANT == 5 ? __builtin_amdgcn_s_memtime()
+                                        : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
 
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *a.overflow_next = 0u;
-    *a.queue_next = 0u;
-    if (a.state_init) {
-      uint64_t* st = (uint64_t*)a.state_init;
-      st[0] = a.init_carry;
-      st[1] = 0;
-      st[2] = 0;
-      st[3] = 0;
-      st[4] = 0;
-      st[5] = 0;
-    }
-  }
+  if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.overflow_next = 0u;  // (the next piece's slot)
   if constexpr (VARIANT == 4) {
     for (int e = threadIdx.x; e < W * STG / 4; e += NT)
       reinterpret_cast<uint32_t*>(lds + kTableBytes)[e] = 0u;
@@ -714,21 +696,40 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   const bool live = region < a.nregions;
   // The first line's DMA is issued before the table fill, so its HBM latency
   // overlaps the fill instead of following it.
+  // The 1 KiB table reaches LDS by one LDS-DMA instruction of wave 0, issued
+  // before the first line's DMA, so waiting for it (vmcnt(8)) does not wait
+  // for the line: the fill overlaps the line's HBM latency.  (A plain load's
+  // use gets a vmcnt(0) from the compiler, which also waits for the line; a
+  // load in inline asm returns into a register the compiler may copy before
+  // the wait -- it did, and the copy read a stale value.)
+  static_assert(NT % 256 == 0, "table fill shape");
+  if (wave == 0) {
+    const uint64_t tp = (uint64_t)(uintptr_t)&kT[0];
+    u32x4 trs;
+    trs.x = __builtin_amdgcn_readfirstlane((uint32_t)tp);
+    trs.y = __builtin_amdgcn_readfirstlane((uint32_t)(tp >> 32) & 0xFFFFu);
+    trs.z = 1024u;
+    trs.w = 0x00020000u;
+    dma16(trs, lane * 16u,
+          __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)s_tab));
+  }
   u32x4 rsrc = {0u, 0u, 0u, 0u};
   uint32_t sh = 0;
-  uint32_t ticket = 0;
   if (live) {
     desc_of(region, rsrc, sh);
-    if (lane == 0) ticket = atomicAdd(a.queue, 1u);
     issue(rsrc, sh, 0u);
   }
-  // one table load per thread (a loop of dependent loads cost ~15 us of the
-  // launch): thread t writes byte value t % 256 into slots of its share
+  if (wave == 0) {
+    if (live && VARIANT != 4)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
   {
-    static_assert(NT % 256 == 0, "table fill shape");
     constexpr int TPV = NT / 256;  // threads per byte value
     const uint32_t v = threadIdx.x & 255u;
-    const uint32_t tv = kT[v];
+    const uint32_t tv = s_tab[v];
     uint2 t;
     t.x = tv;
     t.y = __builtin_amdgcn_alignbit(tv, tv, 16);
@@ -748,14 +749,51 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   uint64_t vm_wait = 0, copy_wait = 0, dma_issue = 0;
   uint32_t nreg_done = 0;
 
+  // Work queue for the regions beyond the first pass (region nstatic + 8t + x
+  // is ticket t of counter x).  Each wave draws from its XCD's counter and
+  // moves on to the next counter once one runs dry; it draws its successor's
+  // ticket in the middle of a region and decodes it at the region's last
+  // line, so the atomic's latency is hidden.  2048 waves drawing from ONE counter at
+  // the launch serialised for ~20 us (profiles/r03/trace_prologue.txt); a
+  // piece with no more regions than wave slots draws nothing.
+  const uint32_t nstatic = gridDim.x * W;
+  bool draw = a.nregions > nstatic;
+  uint32_t qx = 0, qdry = 0;  // current counter, counters found empty
+  if (draw) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    qx = xcc & 7u;
+  }
+  uint32_t ticket = 0;
+
   while (true) {
-    const uint32_t next = gridDim.x * W + __builtin_amdgcn_readfirstlane(ticket);
+    uint32_t next = a.nregions;
     u32x4 nrsrc = rsrc;
     uint32_t nsh = 0;
-    if (next < a.nregions) {
-      if (lane == 0) ticket = atomicAdd(a.queue, 1u);
+    // the successor region (called once, at the region's last line)
+    auto resolve_next = [&]() __attribute__((always_inline)) {
+      if (!draw) return;
+      uint32_t rq = 0;  // lane 0: counter | dry counters << 8
+      uint32_t rr = a.nregions, qq = qx, dry = qdry;
+      if (lane == 0) {  // (lane 0 holds the tickets)
+        uint64_t r = nstatic + 8ull * ticket + qq;
+        while (r >= a.nregions && ++dry < 8u) {  // this counter ran dry: the next one
+          qq = (qq + 1u) & 7u;
+          r = nstatic + 8ull * atomicAdd(a.queue + 32u * qq, 1u) + qq;
+        }
+        rr = r < a.nregions ? (uint32_t)r : a.nregions;
+        rq = qq | (dry << 8);
+      }
+      next = __builtin_amdgcn_readfirstlane(rr);
+      rq = __builtin_amdgcn_readfirstlane(rq);
+      qx = rq & 0xFFu;
+      qdry = rq >> 8;
+      if (next >= a.nregions) {
+        draw = false;
+        return;
+      }
       desc_of(next, nrsrc, nsh);
-    }
+    };
 
     uint32_t cnt = 0;
     uint32_t ereg[kHitRegs] = {};
@@ -806,10 +844,12 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         __builtin_amdgcn_s_setprio(0);
       else
         __builtin_amdgcn_s_setprio(1);
-      if (b + 1u < NB)
+      if (b + 1u < NB) {
         issue(rsrc, sh, b + 1u);
-      else
+      } else {
+        resolve_next();
         issue(nrsrc, nsh, next < a.nregions ? 0u : NB);
+      }
       if constexpr (VARIANT == 5) dma_issue += __builtin_amdgcn_s_memtime() - tw2;
     };
     fetch(0u);
@@ -936,6 +976,9 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     fetch(1u);
     static_for<D>([&](auto gc) __attribute__((always_inline)) { issue_sub(gc); });
     for (uint32_t t = 0; t < M; ++t) {
+      // the successor's ticket, drawn mid-region: waves that started
+      // together reach this point spread out, so the draws do not queue
+      if (t == M / 2u && draw && lane == 0) ticket = atomicAdd(a.queue + 32u * qx, 1u);
       const uint32_t o0 = t * 3u * (uint32_t)kLine;
       static_for<48>([&](auto gc) __attribute__((always_inline)) {
         constexpr int g = decltype(gc)::value;
@@ -1022,11 +1065,15 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (a.trace && lane == 0) {
-    uint64_t* tr = a.trace + 3ull * (blockIdx.x * W + wave);
+    uint64_t* tr = a.trace + 4ull * (blockIdx.x * W + wave);
+    tr[3] = t_entry;
     tr[0] = t_start;
     tr[1] = VARIANT == 5 ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
     // VARIANT 5: {vmcnt wait, line copy + lgkmcnt(0), DMA issue} cycles, 21 bits each
-    tr[2] = VARIANT == 5 ? (vm_wait | (copy_wait << 21) | (dma_issue << 42)) : nreg_done;
+    uint32_t xcc_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_id));
+    tr[2] = VARIANT == 5 ? (vm_wait | (copy_wait << 21) | (dma_issue << 42))
+                         : (nreg_done | ((uint64_t)xcc_id << 32));
   }
 }
 

@@ -90,6 +90,9 @@ struct StitchArgs {
   HostState* host_state;  // pinned, written by fixup_kernel (may be null)
   uint64_t seq;
   uint64_t* trace;        // diagnostics: per walk workgroup 5 timestamps (may be null)
+  uint64_t init_carry;    // init: the chain origin
+  uint32_t init;          // first piece of a call: walk_kernel resets the chain state
+  uint32_t pad_init;
 };
 
 }  // namespace dsx

@@ -266,12 +266,26 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   uint64_t* tr = (a.trace && threadIdx.x == 0) ? a.trace + 10ull * blockIdx.x : nullptr;
   if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
   DevState* st = a.state;
+  // the first piece of a call starts the chain at init_carry: the state is
+  // reset here (block 0) and every workgroup uses the initial values, so no
+  // kernel of another stream (the next piece's scan) touches the state
+  const bool init = a.init != 0;
+  const uint32_t done0 = init ? 0u : st->done;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // for finish_kernel
-    st->base = st->total;
-    st->skip = (st->done || *a.pc.overflow) ? 1u : 0u;
+    if (init) {
+      st->carry = a.init_carry;
+      st->total = 0;
+      st->piece_cuts = 0;
+      st->repaired = 0;
+      st->done = 0;
+      st->err = 0;
+      st->active = 0;
+    }
+    st->base = init ? 0ull : st->total;
+    st->skip = (done0 || *a.pc.overflow) ? 1u : 0u;
   }
-  if (st->done || *a.pc.overflow) return;  // finished, or scan lists overflowed
-  const uint64_t s0 = uniform64(st->carry);  // scalar: the walks below are wave-uniform
+  if (done0 || *a.pc.overflow) return;  // finished, or scan lists overflowed
+  const uint64_t s0 = init ? a.init_carry : uniform64(st->carry);  // scalar: wave-uniform walks
   const uint32_t kA = blockIdx.x * a.spg;
   if (kA >= a.nseg) return;
   const uint32_t kB = (kA + a.spg < a.nseg ? kA + a.spg : a.nseg) - 1;  // inclusive

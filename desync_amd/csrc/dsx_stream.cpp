@@ -126,7 +126,7 @@ int st_issue(dsx_ctx* c, uint64_t len, bool last) {
   HIPCHK(c, hipMemcpyAsync(s.dbuf[slot].p, s.h + (P - halo - s.hbase), halo + len,
                            hipMemcpyHostToDevice, c->copy_stream));
   HIPCHK(c, hipEventRecord(s.copy_ev[slot], c->copy_stream));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, s.copy_ev[slot], 0));
+  HIPCHK(c, scan_wait(c, s.copy_ev[slot]));  // the scan reads the batch (the stitch follows it)
   // the batch's entry cut (the digest range starts there) and, for a carried
   // chain, its cut count restarting at 0 (the batch's cuts start at out[0])
   uint64_t* rng = s.rng.p + 4 * slot;
@@ -451,8 +451,9 @@ extern "C" const uint8_t* dsx_stream_chunk_data(dsx_ctx_t* c) { return c ? c->st
 
 extern "C" int dsx_stream_pop_many(dsx_ctx_t* c, uint64_t* ends, uint8_t* ids, uint64_t cap,
                                    uint64_t* start, uint64_t* n) {
-  if (!c || !start || !n || (cap && !ends)) return DSX_E_INVAL;
+  if (!c || !start || !n || !cap || !ends) return DSX_E_INVAL;  // (nothing is popped)
   *n = 0;
+  if (ids && c->st.ids < 0) return DSX_E_STATE;  // IDs were not switched on
   uint64_t size = 0;
   int rc = dsx_stream_pop(c, start, &size);  // collects a batch if needed
   if (rc <= 0) return rc;
@@ -469,10 +470,18 @@ extern "C" int dsx_stream_pop_many(dsx_ctx_t* c, uint64_t* ends, uint8_t* ids, u
       memcpy(id.data(), s.last_id, 32);
       s.grp_ids.push_back(id);
     }
-    if (ids) {
-      if (!s.has_id) return k ? 1 : DSX_E_STATE;  // (IDs were not switched on)
-      memcpy(ids + 32 * k, s.last_id, 32);
+    if (ids && !s.has_id) {
+      // a chunk without an ID where IDs are asked for: the group ends before
+      // it and the chunk goes back to the queue (nothing popped is lost)
+      s.last_chunk = s.h + (first - s.hbase);
+      s.pin = first;
+      s.grp_ids.clear();  // (unpop then re-queues ends alone)
+      rc = dsx_stream_unpop(c, k ? ends[k - 1] : first);
+      if (rc) return rc;
+      *n = k;
+      return k ? 1 : DSX_E_STATE;
     }
+    if (ids) memcpy(ids + 32 * k, s.last_id, 32);
     ++k;
     if (k >= cap || s.cuts.empty()) break;
     uint64_t st0, sz;

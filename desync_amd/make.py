@@ -190,11 +190,61 @@ class _CancelWatch:
         return False
 
 
+def _run_polled(fn, dctx, progress):
+    """Runs the library call ``fn`` and, with a ``progress`` callback, reports
+    dsx_progress to it from THIS thread while the call runs on a worker thread
+    (ctypes releases the GIL), as IndexFromFile's main goroutine calls
+    pb.Set per assembled chunk (make.go:134-140)."""
+    if progress is None:
+        return fn()
+    import threading
+    res = {}
+
+    def work():
+        try:
+            res["rc"] = fn()
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            res["exc"] = e
+
+    t = threading.Thread(target=work, daemon=True)
+    t.start()
+    v, last = ctypes.c_uint64(), 0
+    while True:
+        t.join(0.002)
+        if lib().dsx_progress(dctx.h, ctypes.byref(v)) == 0 and v.value > last:
+            last = v.value
+            progress(last)
+        if not t.is_alive():
+            break
+    if "exc" in res:
+        raise res["exc"]
+    return res["rc"]
+
+
+def _partial_error(rc, dctx, **partial):
+    """Interrupted (make.go:201-203) or the I/O error, carrying the confirmed
+    prefix the library returned with it (make.go:133-162 returns the chunks
+    assembled so far next to the error)."""
+    if rc == _lib.DSX_E_INTERRUPTED:
+        err = Interrupted()
+    else:
+        try:
+            check(rc, dctx.h)
+        except _lib.DsxError as e:
+            err = e
+    for k, v in partial.items():
+        setattr(err, k, v)
+    return err
+
+
 def index_fd(fd, min_size, avg_size, max_size, offset=0, length=None, algo=None, ctx=None,
-             device=0, cancel=None):
+             device=0, cancel=None, progress=None):
     """dsx_index_fd: a file range -> (chunk end offsets relative to ``offset``,
     uint8 array of 32-byte chunk IDs), both computed on the GPU.  ``length``
-    None means to the end (files and block devices)."""
+    None means to the end (files and block devices).  ``progress(bytes)`` is
+    called with the end of the last confirmed chunk as the call advances.  On
+    cancellation (Interrupted) or a read error (DsxError DSX_E_IO) the raised
+    exception carries the confirmed prefix as ``.ends`` / ``.ids``."""
     p = Params(min_size, avg_size, max_size)
     code = _digest_code(algo)
     size = length if length is not None else max(0, file_size(fd) - offset)
@@ -205,10 +255,11 @@ def index_fd(fd, min_size, avg_size, max_size, offset=0, length=None, algo=None,
 
     def call(c):
         with _CancelWatch(cancel, c):
-            rc = lib().dsx_index_fd(c.h, fd, offset, size, ctypes.byref(p.c), code,
-                                    ends.ctypes.data, ids.ctypes.data, cap, ctypes.byref(n))
-        if rc == _lib.DSX_E_INTERRUPTED:
-            raise Interrupted()
+            rc = _run_polled(lambda: lib().dsx_index_fd(
+                c.h, fd, offset, size, ctypes.byref(p.c), code, ends.ctypes.data,
+                ids.ctypes.data, cap, ctypes.byref(n)), c, progress)
+        if rc in (_lib.DSX_E_INTERRUPTED, _lib.DSX_E_IO):
+            raise _partial_error(rc, c, ends=ends[:n.value].copy(), ids=ids[:n.value].copy())
         check(rc, c.h)
 
     if ctx is not None:
@@ -296,6 +347,11 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
     result, as in the reference.  ``ctx`` mirrors the Go context: any object
     with a ``done()`` method (or None); when it reports done the call stops
     between 64 MiB pieces and Interrupted is raised (make.go:201-203).
+    ``pb.Set`` receives the end of the last confirmed chunk while the call
+    runs (dsx_progress), from the calling thread.  The reference returns
+    ``(index, stats, err)``; here an error is raised and carries the chunks
+    assembled before it as ``err.index`` / ``err.stats`` (the confirmed
+    prefix of the chain, with IDs).
     """
     pb = pb or NullProgressBar()
     stats = ChunkingStats()
@@ -304,6 +360,15 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
         flags |= CaFormatSHA512256  # make.go:35-38
     Params(min_size, avg_size, max_size)  # NewChunker validation, make.go:103
     index = Index(FormatIndex(flags, min_size, avg_size, max_size), [])
+
+    def assemble(ends, ids):
+        el = ends.tolist()
+        raw = ids.tobytes()
+        index.Chunks = [IndexChunk(raw[32 * i:32 * i + 32], s, e - s)
+                        for i, (s, e) in enumerate(zip([0] + el[:-1], el))]
+        stats.ChunksAccepted = len(index.Chunks)
+        stats.ChunksProduced = len(index.Chunks)
+
     with open(name, "rb") as f:
         head = f.read(64)
         index.Index.FeatureFlags |= catar_feature_flags(head)  # make.go:49-61
@@ -312,16 +377,24 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
         pb.Start()
         try:
             if ctx is not None and getattr(ctx, "done", lambda: False)():
-                raise Interrupted()
-            ends, ids = index_fd(f.fileno(), min_size, avg_size, max_size, 0, size,
-                                 device=device, cancel=ctx)
-            el = ends.tolist()
-            raw = ids.tobytes()
-            index.Chunks = [IndexChunk(raw[32 * i:32 * i + 32], s, e - s)
-                            for i, (s, e) in enumerate(zip([0] + el[:-1], el))]
-            pb.Set(size)  # (the data path runs in one library call)
-            stats.ChunksAccepted = len(index.Chunks)
-            stats.ChunksProduced = len(index.Chunks)
+                e = Interrupted()
+                e.index, e.stats = index, stats
+                raise e
+            try:
+                # pb.Set(chunk.Start + chunk.Size) as chunks are confirmed (make.go:138)
+                ends, ids = index_fd(f.fileno(), min_size, avg_size, max_size, 0, size,
+                                     device=device, cancel=ctx, progress=pb.Set)
+            except (Interrupted, _lib.DsxError) as e:
+                # make.go:133-162 returns the chunks assembled so far with the
+                # error: here the raised error carries them (.index, .stats)
+                if getattr(e, "ends", None) is not None:
+                    assemble(e.ends, e.ids)
+                    if len(e.ends):
+                        pb.Set(int(e.ends[-1]))
+                e.index, e.stats = index, stats
+                raise
+            assemble(ends, ids)
+            pb.Set(size)
         finally:
             pb.Finish()
     return index, stats

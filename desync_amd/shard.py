@@ -13,8 +13,9 @@ seam that does not converge inside its window (a zero run across a shard
 boundary -- README.md:114-119) makes its owner re-walk its shard from the
 true entry cut over its kept candidate lists (no byte is scanned again); the
 ranks then exchange the records again (DSX_E_RESYNC; at most nranks rounds).
-A rank whose resolve fails marks its record DSX_SEAM_ERROR and publishes it
-once more, so every peer fails too instead of waiting (DSX_E_PEER).
+Every round ends with a one-integer all-reduce of the ranks' outcomes, so a
+rank whose resolve fails makes every peer fail in the same round instead of
+leaving one rank waiting in a collective (PeerFailed).
 
 Chunk IDs across seams (shard_chunk_ids): the chunk that ends at a rank's
 first cut starts in an earlier shard, at most max bytes back; the ranks
@@ -71,27 +72,50 @@ def failed_ranks(all_bytes: bytes, world: int):
                               "little") & _lib.DSX_SEAM_ERROR]
 
 
+# round outcomes, agreed as their maximum over the ranks
+AGREE_OK, AGREE_RESYNC, AGREE_FAIL = 0, 1, 2
+
+
+def agree_max(code, group=None, device=None):
+    """max(code) over the ranks of ``group`` (one tiny all-reduce)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(code)], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
 def seam_protocol(engine, world, rec=None):
     """The exchange / resolve loop (dsx.h, multi-GPU shards).  ``engine``:
     local() -> record; exchange(record) -> all records; failed(all) -> ranks
     with DSX_SEAM_ERROR; resolve(all) -> "ok" | "resync" (raises on a local
-    failure); record() -> the (re-walked) record; mark_error(record) ->
-    record with DSX_SEAM_ERROR; result() -> this rank's cut list."""
+    failure); agree(code) -> the maximum of the ranks' AGREE_* codes;
+    record() -> the (re-walked) record; result() -> this rank's cut list.
+
+    Every round ends with agree(): a rank whose resolve fails (or that sees a
+    DSX_SEAM_ERROR record) contributes AGREE_FAIL, so every rank learns of the
+    failure in the same round and raises -- nobody returns while a peer waits
+    in a collective that will never be joined.  Resolve outcomes
+    are a function of the gathered records, so the ranks agree on "ok" /
+    "resync" unless one of them failed."""
     rec = engine.local() if rec is None else rec
     for _ in range(world + 1):
         allrec = engine.exchange(rec)
         bad = engine.failed(allrec)
+        err = None
         if bad:
-            raise PeerFailed(f"rank(s) {bad} failed during seam resolution")
-        try:
-            st = engine.resolve(allrec)
-        except PeerFailed:
-            raise
-        except BaseException:
-            # let the peers see the failure instead of waiting for this rank
-            engine.exchange(engine.mark_error(rec))
-            raise
-        if st == "ok":
+            code, err = AGREE_FAIL, PeerFailed(f"rank(s) {bad} failed during seam resolution")
+        else:
+            try:
+                code = AGREE_RESYNC if engine.resolve(allrec) == "resync" else AGREE_OK
+            except BaseException as e:  # noqa: BLE001 -- re-raised after the agreement
+                code, err = AGREE_FAIL, e
+        agreed = engine.agree(code)
+        if err is not None:
+            raise err
+        if agreed == AGREE_FAIL:
+            raise PeerFailed("a peer rank failed during seam resolution")
+        if agreed == AGREE_OK:
             return engine.result()
         rec = engine.record()
     raise RuntimeError("seam resolution did not settle within nranks rounds")
@@ -134,6 +158,9 @@ class _HostEngine:
 
     def failed(self, allrec):
         return failed_ranks(allrec, self.world)
+
+    def agree(self, code):
+        return agree_max(code, self.group, self.device)
 
     def resolve(self, allrec):
         arr = seams_from_bytes(allrec, self.world)
@@ -213,6 +240,10 @@ class DeviceShard:
         # the records stay in HBM: dsx_shard_resolve checks their flags on the
         # device and returns DSX_E_PEER (no host round trip per step)
         return []
+
+    def agree(self, code):
+        import torch
+        return agree_max(code, self.group, torch.device("cuda", self.ctx.device) if self.nccl else None)
 
     def resolve(self, allrec):
         rc = lib().dsx_shard_resolve(self.ctx.h, ctypes.c_void_p(allrec.data_ptr()), self.world,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSX_ABI_VERSION 2
+#define DSX_ABI_VERSION 3
 
 /* ---- error codes (negative) ---------------------------------------------- */
 enum {
@@ -91,6 +91,14 @@ int dsx_ctx_destroy(dsx_ctx_t *ctx);
 const char *dsx_last_error(dsx_ctx_t *ctx);
 /* Request cancellation of the running/next call; it returns DSX_E_INTERRUPTED. */
 int dsx_cancel(dsx_ctx_t *ctx);
+/* Progress of the running (or last) dsx_index_* / dsx_cut_fd / dsx_cut_host
+ * call: *bytes = the end of the last confirmed chunk, relative to the call's
+ * `off` -- pb.Set(chunk.Start + chunk.Size) per assembled chunk in
+ * IndexFromFile (make.go:134-140).  Monotone within a call, the file length
+ * once it succeeded.  Like dsx_cancel, safe to call from another thread while
+ * the call runs (it reads pinned memory the device publishes into after each
+ * 256 MiB piece; it never touches the context's streams). */
+int dsx_progress(dsx_ctx_t *ctx, uint64_t *bytes);
 
 /* ---- one-shot cut lists ------------------------------------------------------ */
 #define DSX_OUT_HOST 0u   /* out_ends is host memory */
@@ -301,7 +309,13 @@ int dsx_chunk_ids(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, uint64_t sta
  * out_ends: chunk END offsets relative to off (cap entries); ids: 32 bytes per
  * chunk (cap * 32 bytes); both host memory.  DSX_E_CAPACITY sets *n_out to the
  * required count (len/min + 2 always suffices).  Synchronous; dsx_cancel()
- * interrupts it between 64 MiB pieces (DSX_E_INTERRUPTED). */
+ * interrupts it between 64 MiB pieces (DSX_E_INTERRUPTED).
+ * Partial results (IndexFromFile returns the chunks assembled so far with
+ * chunkErr or Interrupted{}, make.go:133-162, :201-203): on DSX_E_INTERRUPTED
+ * and DSX_E_IO, out_ends / ids hold the confirmed prefix of the chain (every
+ * chunk of the pieces stitched before the stop, with its ID) and *n_out its
+ * length (0 if no piece was done).  dsx_cut_fd / dsx_cut_host do the same
+ * with the cut list alone. */
 int dsx_index_fd(dsx_ctx_t *ctx, int fd, uint64_t off, uint64_t len, const dsx_params_t *p,
                  int algo, uint64_t *out_ends, uint8_t *ids, uint64_t cap, uint64_t *n_out);
 int dsx_index_host(dsx_ctx_t *ctx, const void *h_blob, uint64_t len, const dsx_params_t *p,

@@ -185,6 +185,121 @@ def test_index_cancel_and_io_error(tmp_path):
         ctx.close()
 
 
+class _RecordingBar:
+    """A ProgressBar (progress.go:7-15) that records its calls."""
+
+    def __init__(self):
+        self.calls = []
+
+    def SetTotal(self, total):
+        self.calls.append(("SetTotal", total))
+
+    def Start(self):
+        self.calls.append(("Start",))
+
+    def Set(self, v):
+        self.calls.append(("Set", v))
+
+    def Finish(self):
+        self.calls.append(("Finish",))
+
+    def sets(self):
+        return [c[1] for c in self.calls if c[0] == "Set"]
+
+
+def test_index_progress(tmp_path, monkeypatch):
+    """a14: IndexFromFile calls pb.Set while the data path runs (make.go:138,
+    per assembled chunk): every value is the end of a confirmed chunk, the
+    values never decrease, there is more than one before the end, and the
+    last is the file size; SetTotal/Start first, Finish last."""
+    import desync_amd
+    monkeypatch.setenv("DSX_INDEX_WINDOW", str(4 << 20))
+    monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 20))
+    data = o.synth_uniform(43, 0, (192 << 20) + 12345)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    pb = _RecordingBar()
+    desync_amd._lib.reset_context_pool()  # (the pooled contexts read the env when created)
+    try:
+        index, stats = desync_amd.IndexFromFile(None, str(f), 4, MIN, AVG, MAX, pb=pb)
+    finally:
+        desync_amd._lib.reset_context_pool()
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    assert [c.Start + c.Size for c in index.Chunks] == ref.tolist()
+    sets = pb.sets()
+    assert pb.calls[0] == ("SetTotal", data.size) and pb.calls[1] == ("Start",)
+    assert pb.calls[-1] == ("Finish",) and sets[-1] == data.size
+    assert sets == sorted(sets) and len(set(sets)) >= 2, sets[:20]
+    ends = set(ref.tolist())
+    assert all(v in ends for v in sets), [v for v in sets if v not in ends][:5]
+
+
+def test_index_partial_on_io_error(tmp_path, monkeypatch):
+    """A read error mid-file (the range runs past the end of the file): the
+    error carries the confirmed prefix -- IndexFromFile returns the chunks
+    assembled so far with chunkErr (make.go:133-162) -- cut for cut the
+    oracle's chain and ID for ID hashlib."""
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_INDEX_WINDOW", str(1 << 20))
+    monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 18))
+    data = o.synth_uniform(44, 0, (24 << 20) + 5)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    ctx = _lib.Context(0)
+    fd = os.open(str(f), os.O_RDONLY)
+    try:
+        for algo in ("sha512-256", "sha256"):
+            with pytest.raises(_lib.DsxError) as ei:
+                desync_amd.index_fd(fd, MIN, AVG, MAX, length=data.size + (3 << 20), ctx=ctx,
+                                    algo=algo)
+            e = ei.value
+            assert e.code == _lib.DSX_E_IO
+            n = len(e.ends)
+            assert 0 < n < ref.size and np.array_equal(e.ends, ref[:n])
+            assert int(e.ends[-1]) > data.size - 4 * MAX - (2 << 20)
+            assert [bytes(x) for x in e.ids] == _ids(data, ref[:n], algo)
+            # the next call on the context is unaffected
+            ends, _ = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+            assert np.array_equal(ends, ref)
+    finally:
+        os.close(fd)
+        ctx.close()
+
+
+def test_index_partial_on_cancel(tmp_path, monkeypatch):
+    """Interrupted mid-file (make.go:201-203): cancelled from the progress
+    callback at the first confirmed chunk, IndexFromFile raises Interrupted
+    carrying a non-empty strict prefix of the chain with its IDs."""
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_INDEX_WINDOW", str(8 << 20))
+    monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 20))
+    data = o.synth_uniform(45, 0, 768 << 20)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ctx = _lib.Context(0)
+    fd = os.open(str(f), os.O_RDONLY)
+
+    def cancel_at_first(v):
+        if v > 0:
+            _lib.lib().dsx_cancel(ctx.h)
+
+    try:
+        with pytest.raises(desync_amd.Interrupted) as ei:
+            desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx, progress=cancel_at_first)
+    finally:
+        os.close(fd)
+        ctx.close()
+    e = ei.value
+    n = len(e.ends)
+    ref = o.chunk_stream(data[:int(e.ends[-1]) + 4 * MAX] if n else data[:1], MIN, AVG, MAX)
+    assert 0 < n and int(e.ends[-1]) < data.size
+    assert np.array_equal(e.ends, ref[:n])
+    assert [bytes(x) for x in e.ids] == _ids(data, e.ends)
+
+
 def test_chunk_ids_rejects_malformed_ends(dctx):
     """host ends are validated (order, bounds) before any launch."""
     import torch

@@ -78,3 +78,43 @@ def test_chunk_storage_dedup_and_retry():
     s2 = ChunkStorage(ws2)
     s2.StoreChunk(b)
     assert ws2.chunks == {b"b" * 32: b"y"}
+
+
+def test_legacy_hash_type():
+    """chunker.go:320-371 (NewHash / Initialize / Roll / IsBoundary / Reset):
+    after Initialize on a 48-byte window and Roll over the following bytes,
+    the value is the window hash at every position (the oracle's
+    restatement), and IsBoundary marks exactly the oracle's candidates."""
+    import numpy as np
+
+    from desync_amd.hash import NewHash, hashTable
+    from oracle import oracle as o
+    assert list(hashTable) == [int(v) for v in o.T]
+    data = o.synth_uniform(9, 0, 20000)
+    d = o.discriminator(1024)  # dense enough to see boundaries in 20 kB
+    h = NewHash(48, d)
+    h.Initialize(data[:48].tobytes())
+    assert h.value == o.window_hash(data[:48])
+    got = [48] if h.IsBoundary() else []
+    for p in range(48, data.size):
+        h.Roll(int(data[p]))
+        if p % 997 == 0:
+            assert h.value == o.window_hash(data[p - 47:p + 1])
+        if h.IsBoundary():
+            got.append(p + 1)
+    assert got == o.candidates_np(data, d).tolist() and len(got) > 5
+    h.Reset()
+    assert h.value == 0 and h.idx == 0
+    # a window size other than 48 (Roll rotates the outgoing term by size)
+    g = NewHash(16, 7)
+    g.Initialize(bytes(range(16)))
+    ref = 0
+    for i, c in enumerate(range(16)):
+        ref ^= o.rotl32(int(o.T[c]), 15 - i)
+    assert g.value == ref
+    g.Roll(200)
+    ref2 = 0
+    for i, c in enumerate(list(range(1, 16)) + [200]):
+        ref2 ^= o.rotl32(int(o.T[c]), 15 - i)
+    assert g.value == ref2
+    assert isinstance(g.IsBoundary(), (bool, np.bool_))

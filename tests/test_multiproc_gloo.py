@@ -92,12 +92,8 @@ class OracleEngine:
     def record(self):
         return self.sh.seam_to_bytes(_to_struct(self.rec))
 
-    def mark_error(self, rec):
-        from desync_amd import _lib
-        b = bytearray(rec)
-        off = self.sh.FLAGS_OFF
-        b[off:off + 4] = (int.from_bytes(b[off:off + 4], "little") | _lib.DSX_SEAM_ERROR).to_bytes(4, "little")
-        return bytes(b)
+    def agree(self, code):
+        return self.sh.agree_max(code)
 
     def result(self):
         return self.mine
@@ -167,10 +163,12 @@ def test_seam_protocol_gloo(kind, world):
         assert rounds > 1  # the re-walk path ran
 
 
+@pytest.mark.parametrize("kind", ["seam-zero-run", "random"])
 @pytest.mark.parametrize("world,fail_rank", [(2, 1), (3, 0), (3, 2)])
-def test_seam_protocol_failure_propagates(world, fail_rank):
-    """One rank's resolve fails: it publishes DSX_SEAM_ERROR in one more
-    exchange, every other rank raises PeerFailed; nobody hangs."""
-    msgs = _run(_compose("seam-zero-run"), world, fail_rank)
+def test_seam_protocol_failure_propagates(world, fail_rank, kind):
+    """One rank's resolve fails: the round's agreement tells every other rank,
+    which raises PeerFailed; nobody hangs.  "random" data settles in round 1
+    (the peers' own resolves say "ok"), "seam-zero-run" needs re-walks."""
+    msgs = _run(_compose(kind), world, fail_rank)
     kinds = sorted((m[1], m[0]) for m in msgs)
     assert kinds == [(r, "own" if r == fail_rank else "peer") for r in range(world)]

@@ -29,15 +29,17 @@ for i in range(3):
     print(f"scan_trace: call {i}", flush=True)
     desync_amd.cut_device(t.data_ptr(), n, 16384, 65536, 262144, ctx=ctx)
 st = ctx.stats()
+st_scan_ms, st_stitch_ms = st.scan_ms, st.stitch_ms
 print(f"stats: chunks {st.chunks} candidates {st.candidates} repaired {st.repaired_segments} "
       f"dense {st.dense_fallbacks}")
 ns, nw = ctypes.c_uint64(), ctypes.c_uint64()
 _lib.check(L.dsx_debug_trace(ctx.h, None, 0, ctypes.byref(ns), ctypes.byref(nw)), ctx.h)
-buf = np.zeros(3 * ns.value + 10 * nw.value, np.uint64)
+buf = np.zeros(4 * ns.value + 10 * nw.value, np.uint64)
 _lib.check(L.dsx_debug_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(ns),
                              ctypes.byref(nw)), ctx.h)
-tr = buf[:3 * ns.value].reshape(-1, 3).astype(np.int64)
-wk = buf[3 * ns.value:].reshape(-1, 10).astype(np.int64)
+tr = buf[:4 * ns.value].reshape(-1, 4).astype(np.int64)
+wk = buf[4 * ns.value:].reshape(-1, 10).astype(np.int64)
+gid = np.arange(len(tr))[tr[:, 1] > 0]  # blockIdx * W + wave of the live waves
 tr = tr[tr[:, 1] > 0]
 if os.environ.get("DSX_SCAN_VARIANT") == "5":
     # shader-clock cycles per wave and cycles spent waiting for the line DMA
@@ -53,13 +55,32 @@ if os.environ.get("DSX_SCAN_VARIANT") == "5":
 t0 = tr[:, 0].min()
 st = (tr[:, 0] - t0) / 100.0  # us (100 MHz)
 en = (tr[:, 1] - t0) / 100.0
-print(f"waves {len(tr)}  regions/wave {np.bincount(tr[:, 2].astype(int)).tolist()}")
+ent = (tr[:, 3] - t0) / 100.0
+xcc = (tr[:, 2] >> 32) & 0xF
+nreg = tr[:, 2] & 0xFFFFFFFF
+print(f"waves {len(tr)}  regions/wave {np.bincount(nreg.astype(int)).tolist()}")
 q = [0, 1, 10, 50, 90, 99, 100]
+print(f"HIP-event scan ms of the traced call {st_scan_ms:.4f}, stitch ms {st_stitch_ms:.4f}; "
+      f"first wave entry -> last wave end {en.max() - ent.min():.1f} us")
+print("entry us  pct", q, np.percentile(ent, q).round(1).tolist())
+print("prologue (entry -> hashing start) us pct", q, np.percentile(st - ent, q).round(1).tolist())
 print("start us  pct", q, np.percentile(st, q).round(1).tolist())
 print("end   us  pct", q, np.percentile(en, q).round(1).tolist())
-wi = np.arange(len(tr)) % W
+wi = gid % W
 for w in range(W):
     print(f"  wave {w}: end median {np.median(en[wi == w]):7.1f}  max {en[wi == w].max():7.1f}")
+full = nreg == np.bincount(nreg.astype(int)).argmax()  # waves with the common region count
+for x in range(8):
+    m = full & (xcc == x)
+    if m.any():
+        print(f"  xcc {x}: waves {m.sum():4d} end pct [10, 50, 90] "
+              f"{np.percentile(en[m], [10, 50, 90]).round(1).tolist()}")
+wg = gid // W
+wg_end = np.array([en[(wg == g) & full].mean() if ((wg == g) & full).any() else np.nan
+                   for g in range(wg.max() + 1)])
+print("per-workgroup mean end us pct", q, np.nanpercentile(wg_end, q).round(1).tolist())
+wsd = np.array([en[(wg == g) & full].std() for g in range(wg.max() + 1) if ((wg == g) & full).sum() > 1])
+print("within-workgroup end std us pct", [10, 50, 90], np.percentile(wsd, [10, 50, 90]).round(2).tolist())
 wk = wk[wk[:, 4] > 0]
 if len(wk):
     rel = (wk[:, :5] - t0) / 100.0
