@@ -179,7 +179,10 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
-  if (const char* v = getenv("DSX_SCAN_TRACE")) c->scan_trace = atoi(v) != 0;
+  if (const char* v = getenv("DSX_SCAN_TRACE")) {
+    c->scan_trace = atoi(v) != 0;
+    c->trace_keep = atoi(v) == 2;  // keep the traces of the last 4 pieces (slot = seq % 4)
+  }
   if (const char* v = getenv("DSX_WAVE_MAJOR")) c->wave_major = atoi(v) != 0;
   if (const char* v = getenv("DSX_FIXUP_FAST")) c->fixup_fast = atoi(v) != 0;
   if (const char* v = getenv("DSX_FINISH")) c->finish = atoi(v) != 0;
@@ -195,15 +198,29 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
   }
   if (const char* v = getenv("DSX_STITCH_CUS")) c->stitch_cus = std::max(0, std::min(c->ncu / 2, atoi(v)));
+  if (const char* v = getenv("DSX_SCAN_MASK")) c->scan_mask = atoi(v) != 0;
   CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   c->scan_stream = c->stream;
   if (c->stitch_cus > 0) {
-    // the scans' CU mask leaves the last stitch_cus CUs to the stitch kernels
-    std::vector<uint32_t> mask((c->ncu + 31) / 32, 0u);
-    for (int i = 0; i < c->ncu - c->stitch_cus; ++i) mask[i / 32] |= 1u << (i % 32);
+    // The scan's grid leaves stitch_cus CUs free (one per XCD at 8), and its
+    // stream has the highest priority, so the dispatcher places a scan's
+    // workgroups ahead of a concurrent stitch's, which fills the free CUs.
+    // (A CU mask instead -- bit i is a CU of XCD i % 8 -- left one shader
+    // engine per XCD a CU short of its round-robin share of the grid: a few
+    // workgroups started only after the others ended, 1.9x the scan time.)
     hipStream_t ss = nullptr;
-    CREATE_STEP(hipExtStreamCreateWithCUMask(&ss, (uint32_t)mask.size(), mask.data()));
+    if (c->scan_mask) {
+      std::vector<uint32_t> mask((c->ncu + 31) / 32, 0u);
+      for (int i = 0; i < c->ncu - c->stitch_cus; ++i) mask[i / 32] |= 1u << (i % 32);
+      CREATE_STEP(hipExtStreamCreateWithCUMask(&ss, (uint32_t)mask.size(), mask.data()));
+    } else {
+      int least = 0, greatest = 0;
+      CREATE_STEP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      const char* pv = getenv("DSX_SCAN_PRIO");
+      CREATE_STEP(hipStreamCreateWithPriority(&ss, hipStreamNonBlocking,
+                                              pv && atoi(pv) == 0 ? least : greatest));
+    }
     c->scan_stream = ss;
     for (int i = 0; i < 2; ++i) {
       CREATE_STEP(hipEventCreateWithFlags(&c->ev_scan[i], hipEventDisableTiming));
@@ -298,7 +315,8 @@ extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64
   if (!c || !n_scan || !n_walk) return DSX_E_INVAL;
   *n_scan = c->trace_n;
   *n_walk = c->trace_walk_n;
-  const uint64_t words = 4 * c->trace_n + 10 * c->trace_walk_n;
+  const uint64_t words = c->trace_keep ? 4 * (kScanTraceWords * c->trace_n + 10 * 65536ull)
+                                       : kScanTraceWords * c->trace_n + 10 * c->trace_walk_n;
   if (!words || !out) return DSX_OK;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -385,7 +403,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     // (up to two trips past the target when that keeps every region in the
     // first pass: a second pass for a few regions costs a whole region time)
     const uint64_t mcap = c->lane_target / (3 * kLine);
-    if (m > mcap + 2 || rounds_needed > 1) m = std::min<uint64_t>(m, mcap);
+    if (m > mcap + mcap / 4 || rounds_needed > 1) m = std::min<uint64_t>(m, mcap);
     m = std::max<uint64_t>(1, std::min<uint64_t>(m, kLineLaneMax / (3 * kLine)));
     S = (uint32_t)(3 * kLine * m);
     if (c->lane_bytes_override && c->lane_bytes_override % (3 * kLine) == 0 &&
@@ -489,9 +507,11 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   c->last_grid_P = line ? P - delta : P;
   if (c->scan_trace && line) {
     c->trace_n = (uint64_t)c->ncu * W;
-    HIPCHK(c, grow(c, c->trace, 4 * c->trace_n + 10 * 65536));
-    HIPCHK(c, hipMemsetAsync(c->trace.p, 0, 4 * c->trace_n * sizeof(uint64_t), ss));
-    sa.trace = c->trace.p;
+    const uint64_t slot_words = kScanTraceWords * c->trace_n + 10 * 65536ull;
+    HIPCHK(c, grow(c, c->trace, (c->trace_keep ? 4 : 1) * slot_words));
+    c->trace_base = c->trace_keep ? (seq % 4) * slot_words : 0;
+    HIPCHK(c, hipMemsetAsync(c->trace.p + c->trace_base, 0, kScanTraceWords * c->trace_n * sizeof(uint64_t), ss));
+    sa.trace = c->trace.p + c->trace_base;
   }
   const uint32_t pi = c->npiece_call++;
   while (c->pev.size() < 3 * (size_t)(pi + 1)) {
@@ -621,6 +641,11 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   // segments per walk workgroup: about two workgroups per CU (the walks are
   // latency-bound), within the LDS candidate and region budgets
   uint64_t spg = std::max<uint64_t>(2, nseg / (2ull * (uint64_t)c->ncu));
+  // split streams: the walk runs beside the next piece's scan on the CUs the
+  // scan leaves free, two 1024-thread workgroups per CU (LDS: ~69 KiB each)
+  const bool wide = c->scan_stream != c->stream;
+  if (wide)
+    spg = std::max<uint64_t>(spg, (nseg + 2ull * c->stitch_cus - 1) / (2ull * c->stitch_cus));
   spg = std::min<uint64_t>(spg, (uint64_t)((double)kWalkLdsCap / (2.0 * exp_per_seg)) - 1);
   const uint64_t max_spg_reg = region_bytes ? (4000ull * region_bytes) / seg : kMaxSpg;
   spg = std::min<uint64_t>(spg, max_spg_reg > 2 ? max_spg_reg - 2 : 1);
@@ -652,11 +677,14 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   c->init_pending = false;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
   if (trace && walk_grid <= 65536) {
-    ta.trace = c->trace.p + 4 * c->trace_n;
+    ta.trace = c->trace.p + c->trace_base + kScanTraceWords * c->trace_n;
     c->trace_walk_n = walk_grid;
   }
   const size_t walk_lds = (size_t)kWalkLdsCap * 4 + (kMaxSpg + 1) * 8;
-  hipLaunchKernelGGL(walk_kernel, dim3(walk_grid), dim3(256), walk_lds, c->stream, ta);
+  if (wide)
+    hipLaunchKernelGGL(walk_kernel<1024>, dim3(walk_grid), dim3(1024), walk_lds, c->stream, ta);
+  else
+    hipLaunchKernelGGL(walk_kernel<256>, dim3(walk_grid), dim3(256), walk_lds, c->stream, ta);
   HIPCHK(c, hipGetLastError());
   if (c->finish && nseg <= 2048) {  // fixup + gather over nseg/16 workgroups
     const dim3 fg((uint32_t)((nseg + 15) / 16));
@@ -699,7 +727,10 @@ static int run_device(dsx_ctx* c, const uint8_t* d_blob, uint64_t len, CallCfg c
 int ensure_attr_walk(dsx_ctx* c) {
   static bool done = false;
   if (!done) {
-    HIPCHK(c, hipFuncSetAttribute((const void*)walk_kernel,
+    HIPCHK(c, hipFuncSetAttribute((const void*)walk_kernel<256>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kWalkLdsCap * 4 + (kMaxSpg + 1) * 8)));
+    HIPCHK(c, hipFuncSetAttribute((const void*)walk_kernel<1024>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kWalkLdsCap * 4 + (kMaxSpg + 1) * 8)));
     done = true;

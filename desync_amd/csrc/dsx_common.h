@@ -77,6 +77,7 @@ struct ScanArgs {
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches
 // of one 128-B line per lane, so the ring phase repeats), offsets in u16
 constexpr int kLine = 128;
+constexpr int kScanTraceWords = 6;  // per wave: start, end, info, entry, region-end cycles, region-start waits
 constexpr int kQueueSlots = 4;                  // overflow / queue slots (piece seq mod 4)
 constexpr int kQueueWords = 32 + kQueueSlots * 256;  // overflow words + 4 x 8 queue counters
 constexpr uint32_t kLineLaneMax = 384u * 170u;  // 65280

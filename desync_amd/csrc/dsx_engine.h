@@ -24,6 +24,7 @@ template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ void scan_kernel(ScanArgs a);
 template <int MODE, int VARIANT, int W, int SUB, int D>
 __global__ void scanl_kernel(ScanArgs a);
+template <int NT>
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
 template <int PER>
@@ -94,12 +95,14 @@ struct dsx_ctx {
   int device = 0;
   int ncu = 256;
   hipStream_t stream = nullptr, copy_stream = nullptr;
-  // Scans run on scan_stream, CU-masked to all but `stitch_cus` CUs, and
-  // everything else (the stitch, digests, copies, host syncs) on `stream`: a
-  // piece's stitch then overlaps the next piece's scan on the CUs the scan
-  // leaves free.  stitch_cus == 0: scan_stream == stream.
+  // Scans run on scan_stream (highest priority; their grid leaves
+  // `stitch_cus` CUs free) and everything else (the stitch, digests, copies,
+  // host syncs) on `stream`: a piece's stitch then overlaps the next piece's
+  // scan on the CUs the scan leaves free.  stitch_cus == 0:
+  // scan_stream == stream.
   hipStream_t scan_stream = nullptr;
-  int stitch_cus = 8;                      // DSX_STITCH_CUS
+  int stitch_cus = 0;                      // DSX_STITCH_CUS (experiment, off: DESIGN.md 4.2)
+  bool scan_mask = false;                  // DSX_SCAN_MASK: CU-masked scan stream (experiment)
   hipEvent_t ev_scan[2] = {}, ev_stitch[2] = {};  // per region-list set (piece parity)
   bool timing = true;  // record the per-piece scan/stitch events (stats.scan_ms/stitch_ms)
   std::atomic<int> cancel{0};
@@ -128,6 +131,8 @@ struct dsx_ctx {
   bool fixup_fast = true;             // DSX_FIXUP_FAST=0: fixup_kernel for every piece
   DevBuf<uint64_t> trace;       // [4 * trace_n scan records][10 * trace_walk_n walk records]
   uint64_t trace_n = 0, trace_walk_n = 0;
+  bool trace_keep = false;            // DSX_SCAN_TRACE=2: a trace slot per piece (seq % 4)
+  uint64_t trace_base = 0;            // word offset of the current piece's slot
   uint64_t last_grid_P = 0;           // region grid origin of the last enqueued piece
 
   DevBuf<uint32_t> region_cnt, region_list, overflow, rep_cnt, rep_from, flag_list;

@@ -748,6 +748,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
                                         : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
   uint64_t vm_wait = 0, copy_wait = 0, dma_issue = 0;
   uint32_t nreg_done = 0;
+  // trace: shader-clock cycles from the end of a region's hashing to the
+  // start of the next region, and waited at the first two fetches of a
+  // region other than the first
+  uint64_t re_cyc = 0, rs_wait = 0;
 
   // Work queue for the regions beyond the first pass (region nstatic + 8t + x
   // is ticket t of counter x).  Each wave draws from its XCD's counter and
@@ -817,13 +821,15 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         their = s_prog[partner];
       }
       uint64_t tw = 0;
-      if constexpr (VARIANT == 5) tw = __builtin_amdgcn_s_memtime();
+      const bool rs = a.trace && b <= 1u && nreg_done > 0;
+      if (VARIANT == 5 || rs) tw = __builtin_amdgcn_s_memtime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       uint64_t tw1 = 0;
       if constexpr (VARIANT == 5) {
         tw1 = __builtin_amdgcn_s_memtime();
         vm_wait += tw1 - tw;
       }
+      if (rs) rs_wait += __builtin_amdgcn_s_memtime() - tw;
       const uint8_t* my_row = stage + lane * (uint32_t)kLine;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -1008,6 +1014,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       });
     }
 
+    const uint64_t t_hash_end = a.trace ? __builtin_amdgcn_s_memtime() : 0;
     // ---- region end: compact the lanes' hits into one sorted region list ----
     // valid cut offsets o: piece-relative p = lane_p + o in [1, len] and
     // absolute p >= min_pos (windows reaching before the chain origin)
@@ -1059,21 +1066,25 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     }
     ++nreg_done;
     if (next >= a.nregions) break;
+    if (a.trace) re_cyc += __builtin_amdgcn_s_memtime() - t_hash_end;
     region = next;
     rsrc = nrsrc;
     sh = nsh;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (a.trace && lane == 0) {
-    uint64_t* tr = a.trace + 4ull * (blockIdx.x * W + wave);
+    uint64_t* tr = a.trace + (uint64_t)kScanTraceWords * (blockIdx.x * W + wave);
+    tr[4] = re_cyc;
+    tr[5] = rs_wait;
     tr[3] = t_entry;
     tr[0] = t_start;
     tr[1] = VARIANT == 5 ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
     // VARIANT 5: {vmcnt wait, line copy + lgkmcnt(0), DMA issue} cycles, 21 bits each
-    uint32_t xcc_id;
+    uint32_t xcc_id, hw_id;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
     tr[2] = VARIANT == 5 ? (vm_wait | (copy_wait << 21) | (dma_issue << 42))
-                         : (nreg_done | ((uint64_t)xcc_id << 32));
+                         : (nreg_done | ((uint64_t)xcc_id << 32) | ((uint64_t)((hw_id >> 8) & 0xFF) << 40));
   }
 }
 

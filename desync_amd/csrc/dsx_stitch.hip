@@ -226,8 +226,9 @@ __device__ __forceinline__ uint64_t seg_end(const StitchArgs& a, uint32_t k) {
 constexpr int kWalkThreads = 256;
 constexpr uint32_t kWalkMaxRegions = 4096;  // regions a walk workgroup can stage
 
-// Block-wide exclusive scan of one value per thread (kWalkThreads threads);
-// returns the exclusive prefix, *total gets the block sum.
+// Block-wide exclusive scan of one value per thread (NT threads); returns the
+// exclusive prefix, *total gets the block sum.
+template <int NT>
 __device__ uint32_t walk_block_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t incl = v;
@@ -240,7 +241,7 @@ __device__ uint32_t walk_block_scan(uint32_t v, uint32_t* s_wave, uint32_t* tota
   __syncthreads();
   uint32_t before = 0, all = 0;
 #pragma unroll
-  for (int i = 0; i < kWalkThreads / 64; ++i) {
+  for (int i = 0; i < NT / 64; ++i) {
     const uint32_t t = s_wave[i];
     before += (i < (int)wv) ? t : 0u;
     all += t;
@@ -250,7 +251,12 @@ __device__ uint32_t walk_block_scan(uint32_t v, uint32_t* s_wave, uint32_t* tota
   return before + incl - v;
 }
 
-__global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
+// NT = 256 threads (spread over the chip), or 1024 (split streams: a few
+// workgroups beside the next piece's scan, on the CUs it leaves free, each
+// wave walking several segments)
+template <int NT>
+__global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
+  constexpr int kWalkThreads = NT;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* cand = smem;                         // [a.lds_cap]
   uint64_t* xs = (uint64_t*)(smem + a.lds_cap);  // [kMaxSpg + 1] spec exits
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
         c = c < pc.region_cap ? c : pc.region_cap;
       }
       uint32_t part;
-      const uint32_t ex = walk_block_scan(c, s_wave, &part);
+      const uint32_t ex = walk_block_scan<NT>(c, s_wave, &part);
       if (i < nreg) s_off[i] = total + ex;
       total += part;
     }
@@ -382,7 +388,10 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
   __syncthreads();
   if (tr) {
     tr[3] = __builtin_amdgcn_s_memrealtime();
-    tr[6] = __builtin_amdgcn_s_memtime();
+    uint32_t xcc, hwid;  // where this workgroup ran (XCC, SE/SH/CU)
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    tr[6] = ((uint64_t)xcc << 32) | hwid;
   }
 
   // ---- phase 2: staged chain entering from X_{k-1} (one wave each) ----
@@ -453,6 +462,9 @@ __global__ __launch_bounds__(kWalkThreads) void walk_kernel(StitchArgs a) {
     if (tr) tr[4] = __builtin_amdgcn_s_memrealtime();
   }
 }
+
+template __global__ void walk_kernel<256>(StitchArgs);
+template __global__ void walk_kernel<1024>(StitchArgs);
 
 // ---- K3: validity propagation, sequential repair, scan of counts ----------
 constexpr int kFixThreads = 1024;

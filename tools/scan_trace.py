@@ -34,11 +34,11 @@ print(f"stats: chunks {st.chunks} candidates {st.candidates} repaired {st.repair
       f"dense {st.dense_fallbacks}")
 ns, nw = ctypes.c_uint64(), ctypes.c_uint64()
 _lib.check(L.dsx_debug_trace(ctx.h, None, 0, ctypes.byref(ns), ctypes.byref(nw)), ctx.h)
-buf = np.zeros(4 * ns.value + 10 * nw.value, np.uint64)
+buf = np.zeros(6 * ns.value + 10 * nw.value, np.uint64)
 _lib.check(L.dsx_debug_trace(ctx.h, buf.ctypes.data, buf.size, ctypes.byref(ns),
                              ctypes.byref(nw)), ctx.h)
-tr = buf[:4 * ns.value].reshape(-1, 4).astype(np.int64)
-wk = buf[4 * ns.value:].reshape(-1, 10).astype(np.int64)
+tr = buf[:6 * ns.value].reshape(-1, 6).astype(np.int64)
+wk = buf[6 * ns.value:].reshape(-1, 10).astype(np.int64)
 gid = np.arange(len(tr))[tr[:, 1] > 0]  # blockIdx * W + wave of the live waves
 tr = tr[tr[:, 1] > 0]
 if os.environ.get("DSX_SCAN_VARIANT") == "5":
@@ -63,6 +63,12 @@ q = [0, 1, 10, 50, 90, 99, 100]
 print(f"HIP-event scan ms of the traced call {st_scan_ms:.4f}, stitch ms {st_stitch_ms:.4f}; "
       f"first wave entry -> last wave end {en.max() - ent.min():.1f} us")
 print("entry us  pct", q, np.percentile(ent, q).round(1).tolist())
+multi = nreg > 1
+if multi.any():  # region transitions: shader-clock cycles per transition
+    per = (nreg[multi] - 1).astype(np.float64)
+    print("per region transition, kcycles: region end -> next region pct [10, 50, 90]",
+          np.percentile(tr[multi, 4] / per / 1e3, [10, 50, 90]).round(2).tolist(),
+          " first-fetch waits", np.percentile(tr[multi, 5] / per / 1e3, [10, 50, 90]).round(2).tolist())
 print("prologue (entry -> hashing start) us pct", q, np.percentile(st - ent, q).round(1).tolist())
 print("start us  pct", q, np.percentile(st, q).round(1).tolist())
 print("end   us  pct", q, np.percentile(en, q).round(1).tolist())
@@ -84,8 +90,6 @@ print("within-workgroup end std us pct", [10, 50, 90], np.percentile(wsd, [10, 5
 wk = wk[wk[:, 4] > 0]
 if len(wk):
     rel = (wk[:, :5] - t0) / 100.0
-    cyc = (wk[:, 6] - wk[:, 5]) / np.maximum(1, wk[:, 3] - wk[:, 2]) * 100.0
-    print(f"walk phase 1 shader clock MHz median {np.median(cyc):.0f}")
     print(f"walk workgroups {len(wk)} (times from the first scan wave start, us)")
     for i, name in enumerate(["entry", "counts", "staged", "walk1", "walk2"]):
         print(f"  {name:7s} pct {q} {np.percentile(rel[:, i], q).round(1).tolist()}")
