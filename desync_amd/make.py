@@ -383,7 +383,8 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
             try:
                 # pb.Set(chunk.Start + chunk.Size) as chunks are confirmed (make.go:138)
                 ends, ids = index_fd(f.fileno(), min_size, avg_size, max_size, 0, size,
-                                     device=device, cancel=ctx, progress=pb.Set)
+                                     device=device, cancel=ctx,
+                                     progress=None if isinstance(pb, NullProgressBar) else pb.Set)
             except (Interrupted, _lib.DsxError) as e:
                 # make.go:133-162 returns the chunks assembled so far with the
                 # error: here the raised error carries them (.index, .stats)

@@ -118,3 +118,24 @@ def test_legacy_hash_type():
         ref2 ^= o.rotl32(int(o.T[c]), 15 - i)
     assert g.value == ref2
     assert isinstance(g.IsBoundary(), (bool, np.bool_))
+
+
+def test_chop_batches():
+    """ChopFile's read batches (desync_amd.chop._batches): contiguous chunks
+    up to 64 MiB per batch, a longer chunk alone, a gap starts a new batch;
+    every chunk exactly once, in order."""
+    from desync_amd import chop
+    from desync_amd.index import IndexChunk
+    MiB = 1 << 20
+    sizes = [30 * MiB, 30 * MiB, 10 * MiB, 100 * MiB, 1, 5]
+    chunks, pos = [], 0
+    for s in sizes:
+        chunks.append(IndexChunk(b"\0" * 32, pos, s))
+        pos += s
+    chunks.append(IndexChunk(b"\0" * 32, pos + 7, 3))  # (a gap: a new run)
+    got = list(chop._batches(chunks, pos + 10))
+    assert [i for i, _ in got] == [0, 2, 3, 4, 6]
+    assert [len(b) for _, b in got] == [2, 1, 1, 2, 1]
+    assert [c for _, b in got for c in b] == chunks
+    for _, b in got:
+        assert len(b) == 1 or b[-1].Start + b[-1].Size - b[0].Start <= chop._BATCH

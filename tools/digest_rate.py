@@ -24,6 +24,8 @@ from desync_amd import _lib, make  # noqa: E402
 
 GiB = 1 << 30
 MIN, AVG, MAX = 16 << 10, 64 << 10, 256 << 10
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ratestats import repeat  # noqa: E402
 
 
 def main():
@@ -39,14 +41,10 @@ def main():
         ends = make.cut_device(t.data_ptr(), n, MIN, AVG, MAX, ctx=ctx)
         row = {"gib": gib, "chunks": int(ends.size)}
         for name, algo in (("sha512-256", _lib.DSX_DIGEST_SHA512_256), ("sha256", _lib.DSX_DIGEST_SHA256)):
-            ids = make.chunk_ids(t.data_ptr(), n, ends, 0, ctx=ctx, algo=algo)  # warm-up
-            reps = 5
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                ids = make.chunk_ids(t.data_ptr(), n, ends, 0, ctx=ctx, algo=algo)
-            dt = (time.perf_counter() - t0) / reps
-            row[name + "_gibs"] = round(gib / dt, 2)
-            row[name + "_ms"] = round(dt * 1e3, 3)
+            st, ids = repeat(lambda: make.chunk_ids(t.data_ptr(), n, ends, 0, ctx=ctx, algo=algo), n)
+            row[name + "_gibs"] = st["gibs_median"]
+            row[name + "_ms"] = round(st["s_median"] * 1e3, 3)
+            row[name] = st
             # spot-check a few IDs against hashlib
             starts = np.concatenate([[0], ends[:-1]])
             for i in (0, ends.size // 2, ends.size - 1):

@@ -28,12 +28,8 @@ GiB = 1 << 30
 MIN, AVG, MAX = 16 << 10, 64 << 10, 256 << 10
 
 
-def timed(f, reps):
-    f()  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        r = f()
-    return (time.perf_counter() - t0) / reps, r
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ratestats import repeat  # noqa: E402
 
 
 def main():
@@ -45,14 +41,14 @@ def main():
     torch.cuda.synchronize()  # the generator ran on the library's stream
     data = t.cpu().numpy()
     del t
-    t_host, ends_h = timed(lambda: make.cut_host(data, MIN, AVG, MAX), 5)
+    st_host, ends_h = repeat(lambda: make.cut_host(data, MIN, AVG, MAX), n)
     with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp"), delete=False) as f:
         data.tofile(f)
         path = f.name
     try:
         fd = os.open(path, os.O_RDONLY)
         try:
-            t_fd, ends_f = timed(lambda: make.cut_fd(fd, MIN, AVG, MAX), 5)
+            st_fd, ends_f = repeat(lambda: make.cut_fd(fd, MIN, AVG, MAX), n)
         finally:
             os.close(fd)
     finally:
@@ -61,8 +57,10 @@ def main():
     print(json.dumps({
         "bytes": n,
         "chunks": int(len(ends_h)),
-        "cut_host_gibs": round(n / t_host / GiB, 2),
-        "cut_fd_gibs": round(n / t_fd / GiB, 2),
+        "cut_host_gibs": st_host["gibs_median"],
+        "cut_fd_gibs": st_fd["gibs_median"],
+        "cut_host": st_host,
+        "cut_fd": st_fd,
         "note": "host memory -> pinned H2D pipeline -> scan + stitch -> cut list in host memory",
     }))
 

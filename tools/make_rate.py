@@ -24,6 +24,8 @@ sys.path.insert(0, REPO)
 import desync_amd  # noqa: E402
 
 MIN, AVG, MAX = 16 << 10, 64 << 10, 256 << 10
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ratestats import repeat  # noqa: E402
 
 
 def main():
@@ -40,23 +42,21 @@ def main():
                     k = min(left, 256 << 20)
                     f.write(rng.integers(0, 256, k, dtype=np.uint8).tobytes())
                     left -= k
-            desync_amd.IndexFromFile(None, path, 1, MIN, AVG, MAX)  # warm-up (page cache, context)
-            t0 = time.perf_counter()
-            index, stats = desync_amd.IndexFromFile(None, path, 1, MIN, AVG, MAX)
-            b = io.BytesIO()
-            index.WriteTo(b)
-            dt = time.perf_counter() - t0
+            def make():
+                index, stats = desync_amd.IndexFromFile(None, path, 1, MIN, AVG, MAX)
+                b = io.BytesIO()
+                index.WriteTo(b)
+                return index, stats, b
+
+            st_make, (index, stats, b) = repeat(make, n)
             fdr = os.open(path, os.O_RDONLY)
             try:
-                t1 = time.perf_counter()
-                ends, _ = desync_amd.index_fd(fdr, MIN, AVG, MAX)
-                dt_c = time.perf_counter() - t1
+                st_idx, _ = repeat(lambda: desync_amd.index_fd(fdr, MIN, AVG, MAX), n)
+                st_cut, _ = repeat(lambda: desync_amd.cut_fd(fdr, MIN, AVG, MAX), n)
             finally:
                 os.close(fdr)
             # VerifyIndex over the index just made (dsx_ids_fd: file -> HBM -> IDs)
-            t2 = time.perf_counter()
-            desync_amd.VerifyIndex(None, path, index, 1)
-            dt_v = time.perf_counter() - t2
+            st_ver, _ = repeat(lambda: desync_amd.VerifyIndex(None, path, index, 1), n)
             raw = np.fromfile(path, dtype=np.uint8)
             want = desync_amd.cut_host(raw, MIN, AVG, MAX)
             got = np.array([c.Start + c.Size for c in index.Chunks], dtype=np.uint64)
@@ -66,13 +66,13 @@ def main():
                 assert hashlib.new("sha512_256", piece).digest() == c.ID
             del raw
             rows.append({"gib": gib, "chunks": stats.ChunksAccepted, "caibx_bytes": len(b.getvalue()),
-                         "s": round(dt, 4), "gibs": round(gib / dt, 2),
-                         "index_fd_s": round(dt_c, 4), "index_fd_gibs": round(gib / dt_c, 2),
-                         "verify_s": round(dt_v, 4), "verify_gibs": round(gib / dt_v, 2)})
+                         "gibs": st_make["gibs_median"], "index_fd_gibs": st_idx["gibs_median"],
+                         "cut_fd_gibs": st_cut["gibs_median"], "verify_gibs": st_ver["gibs_median"],
+                         "make": st_make, "index_fd": st_idx, "cut_fd": st_cut, "verify": st_ver})
         finally:
             os.unlink(path)
     print(json.dumps({"tool": "make_rate", "params": "16/64/256 KiB", "digest": "sha512-256",
-                      "rows": rows, "note": "page-cache file -> HBM -> cuts + IDs -> caibx bytes (IndexFromFile); index_fd = the C call alone (dsx_index_fd); verify = VerifyIndex of that index (dsx_ids_fd)"}))
+                      "rows": rows, "note": "page-cache file -> HBM -> cuts + IDs -> caibx bytes (IndexFromFile); index_fd = the C call alone (dsx_index_fd); cut_fd = the cut list alone (dsx_cut_fd); verify = VerifyIndex of that index (dsx_ids_fd); medians of DSX_RATE_REPS (10) runs with min/max"}))
 
 
 if __name__ == "__main__":

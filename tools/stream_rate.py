@@ -23,6 +23,8 @@ import desync_amd  # noqa: E402
 from desync_amd import _lib, make  # noqa: E402
 
 MIN, AVG, MAX = 16 << 10, 64 << 10, 256 << 10
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ratestats import repeat  # noqa: E402
 
 
 def main():
@@ -32,15 +34,13 @@ def main():
     data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
     ctx = _lib.default_context(0)
     want = make.cut_host(np.frombuffer(data, np.uint8), MIN, AVG, MAX, ctx=ctx)
-    best = None
-    for _ in range(3):
-        t0 = time.perf_counter()
-        ch = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX, ctx=ctx)
-        ends = []
-        for start, b in ch:
-            ends.append(start + len(b))
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
+    def run_next(zero_copy):
+        ch = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX, ctx=ctx, zero_copy=zero_copy)
+        return [start + len(b) for start, b in ch]
+
+    st_zc, ends = repeat(lambda: run_next(True), n)
+    st_copy, ends_c = repeat(lambda: run_next(False), n)
+    assert ends == ends_c
     assert np.array_equal(np.array(ends, dtype=np.uint64), want), "stream cut list differs"
 
     class NullStore:  # ChunkStream's store: keeps nothing (stores are out of scope)
@@ -50,25 +50,22 @@ def main():
         def StoreChunk(self, chunk):
             pass
 
-    best_cs = None
-    for _ in range(3):
-        t0 = time.perf_counter()
-        idx = desync_amd.ChunkStream(None, desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX),
-                                     NullStore(), 4)
-        dt = time.perf_counter() - t0
-        best_cs = dt if best_cs is None else min(best_cs, dt)
+    st_cs, idx = repeat(lambda: desync_amd.ChunkStream(
+        None, desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX), NullStore(), 4), n)
     got = np.array([c.Start + c.Size for c in idx.Chunks], dtype=np.uint64)
     assert np.array_equal(got, want), "ChunkStream cut list differs"
     import hashlib
     for c in (idx.Chunks[0], idx.Chunks[-1]):
         assert hashlib.new("sha512_256", data[c.Start:c.Start + c.Size]).digest() == c.ID
     print(json.dumps({"tool": "stream_rate", "mib": mib, "chunks": len(ends),
-                      "gibs": round(n / best / (1 << 30), 2), "s": round(best, 4),
-                      "chunkstream_gibs": round(n / best_cs / (1 << 30), 2),
-                      "chunkstream_s": round(best_cs, 4),
-                      "note": "io.BytesIO reader (readinto into the library's pinned buffer), "
-                              "a zero-copy chunk view per Next; ChunkStream = Next + GPU "
-                              "SHA-512/256 IDs + bytes clone + store call per chunk"}))
+                      "gibs": st_zc["gibs_median"], "next_zero_copy": st_zc,
+                      "next_copy_gibs": st_copy["gibs_median"], "next_copy": st_copy,
+                      "chunkstream_gibs": st_cs["gibs_median"], "chunkstream": st_cs,
+                      "note": "io.BytesIO reader (readinto into the library's pinned buffer); "
+                              "Next with zero_copy views (Go's aliasing rule) and with the "
+                              "default bytes copy; ChunkStream = Next + GPU SHA-512/256 IDs + "
+                              "bytes clone + store call per chunk; medians of DSX_RATE_REPS "
+                              "(10) runs with min/max"}))
 
 
 if __name__ == "__main__":
