@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import io
 import struct
+from collections.abc import MutableSequence
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -43,6 +44,64 @@ class IndexChunk:
     Size: int
 
 
+class ChunkArray(MutableSequence):
+    """Index.Chunks of a contiguous chunk list held as arrays (chunk ends and
+    32-byte IDs, as libdsx returns them): IndexChunk objects are built only
+    when an element is read, and WriteTo packs the arrays directly.  Any
+    change turns it into a plain list of IndexChunk first."""
+
+    def __init__(self, ends, ids):
+        self._ends = np.ascontiguousarray(ends, dtype=np.uint64)
+        self._ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 32)
+        self._list = None
+
+    def _chunk(self, i):
+        e = int(self._ends[i])
+        s = int(self._ends[i - 1]) if i else 0
+        return IndexChunk(self._ids[i].tobytes(), s, e - s)
+
+    def _materialize(self):
+        if self._list is None:
+            el = self._ends.tolist()
+            raw = self._ids.tobytes()
+            self._list = [IndexChunk(raw[32 * i:32 * i + 32], s, e - s)
+                          for i, (s, e) in enumerate(zip([0] + el[:-1], el))]
+        return self._list
+
+    def __len__(self):
+        return len(self._list) if self._list is not None else len(self._ends)
+
+    def __getitem__(self, i):
+        if self._list is not None:
+            return self._list[i]
+        if isinstance(i, slice):
+            return [self._chunk(k) for k in range(*i.indices(len(self._ends)))]
+        n = len(self._ends)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError("chunk index out of range")
+        return self._chunk(i)
+
+    def __iter__(self):
+        return iter(self._materialize())
+
+    def __setitem__(self, i, v):
+        self._materialize()[i] = v
+
+    def __delitem__(self, i):
+        del self._materialize()[i]
+
+    def insert(self, i, v):
+        self._materialize().insert(i, v)
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return f"ChunkArray({len(self)} chunks)"
+
+
 @dataclass
 class Index:
     Index: FormatIndex = field(default_factory=FormatIndex)
@@ -62,7 +121,11 @@ class Index:
         # table items {end offset, ID} (format.go:596-605), packed in one go
         nc = len(self.Chunks)
         items = np.empty(nc, dtype=_ITEM)
-        if nc:
+        ca = self.Chunks if isinstance(self.Chunks, ChunkArray) and self.Chunks._list is None else None
+        if nc and ca is not None:  # arrays as libdsx returned them
+            items["off"] = ca._ends
+            items["id"] = ca._ids.view("S32").reshape(-1)
+        elif nc:
             items["off"] = np.cumsum(np.fromiter((c.Size for c in self.Chunks), np.uint64, nc))
             items["id"] = np.frombuffer(b"".join(bytes(c.ID) for c in self.Chunks), "S32")
         out += items.tobytes()

@@ -24,7 +24,7 @@ from . import _lib, digest
 from ._lib import DSX_OUT_DEVICE, DSX_OUT_HOST, check, lib
 from .chunker import Params
 from .errors import Interrupted
-from .index import CaFormatExcludeNoDump, CaFormatSHA512256, FormatIndex, Index, IndexChunk, \
+from .index import CaFormatExcludeNoDump, CaFormatSHA512256, ChunkArray, FormatIndex, Index, IndexChunk, \
     catar_feature_flags
 
 
@@ -362,10 +362,7 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
     index = Index(FormatIndex(flags, min_size, avg_size, max_size), [])
 
     def assemble(ends, ids):
-        el = ends.tolist()
-        raw = ids.tobytes()
-        index.Chunks = [IndexChunk(raw[32 * i:32 * i + 32], s, e - s)
-                        for i, (s, e) in enumerate(zip([0] + el[:-1], el))]
+        index.Chunks = ChunkArray(ends, ids)  # (IndexChunk objects built on access)
         stats.ChunksAccepted = len(index.Chunks)
         stats.ChunksProduced = len(index.Chunks)
 
