@@ -7,10 +7,12 @@ seed 1, generated on device) chunked with desync's default min/avg/max =
 produces the complete cut list in HBM (scan + stitch, libdsx.so).
 
 N > 1 (one process per GPU, torch.distributed over RCCL): rank r holds bytes
-[r GiB, (r+1) GiB) of an N GiB blob (+64 B halo, regenerated locally), chunks
-it speculatively (dsx_shard_local), all-gathers the small seam records
-(RCCL, in place in HBM), and resolves its final cut list in HBM
-(dsx_shard_resolve) -- weak scaling.
+[r GiB, (r+1) GiB) of an N GiB blob (+64 B halo, regenerated locally; 32 GiB
+of the seed-3 blob per rank with --config5), chunks it speculatively
+(dsx_shard_local), all-gathers the small seam records (RCCL, in place in
+HBM), and resolves its final cut list in HBM (dsx_shard_resolve_async) --
+weak scaling.  The whole step is ordered on the library stream; the host
+waits once per step (dsx_shard_collect).
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -45,31 +47,41 @@ def parse():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--gib", type=float, default=1.0, help="GiB per GPU")
     ap.add_argument("--workload", default="uniform", choices=["uniform", "dedup", "zeros"])
+    ap.add_argument("--seed", type=int, default=0,
+                    help="generator seed (0: 1 for uniform, 2 for dedup)")
+    ap.add_argument("--config5", action="store_true",
+                    help="BASELINE config 5's shard shape: 32 GiB of the seed-3 uniform blob "
+                         "per GPU (256 GiB over 8 GPUs)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the cpu_baseline leg (0: the job's CPU share)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="chunking jobs kept in flight (one library context each), so the "
                          "host's wait for job k overlaps the GPU work of job k+1 (N > 1: "
-                         "pipeline lanes, one host thread and process group each)")
+                         "pipeline lanes, one library context and process group each)")
     ap.add_argument("--check", action="store_true",
                     help="N>1: compare the concatenated per-rank cut lists with one "
                          "dsx_cut_device over the whole blob on rank 0 (small sizes)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config5:
+        args.gib, args.workload, args.seed = 32.0, "uniform", 3
+    if not args.seed:
+        args.seed = 2 if args.workload == "dedup" else 1
+    return args
 
 
-DATA_LABEL = {"uniform": "uniform, splitmix64 seed 1 (dsx_gen_uniform)",
-              "dedup": "dedup, seed 2, 30 % of 1 MiB blocks copy earlier ones (dsx_gen_dedup)",
+DATA_LABEL = {"uniform": "uniform, splitmix64 seed {seed} (dsx_gen_uniform)",
+              "dedup": "dedup, seed {seed}, 30 % of 1 MiB blocks copy earlier ones (dsx_gen_dedup)",
               "zeros": "zeros"}
 
 
-def make_blob(ctx, t, offset, n, workload):
+def make_blob(ctx, t, offset, n, workload, seed):
     from desync_amd import _lib
     L = _lib.lib()
     if workload == "uniform":
-        _lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), offset, n, 1), ctx.h)
+        _lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), offset, n, seed), ctx.h)
     elif workload == "dedup":
-        _lib.check(L.dsx_gen_dedup(ctx.h, ctypes.c_void_p(t.data_ptr()), offset, n, 2, 0.30),
+        _lib.check(L.dsx_gen_dedup(ctx.h, ctypes.c_void_p(t.data_ptr()), offset, n, seed, 0.30),
                    ctx.h)
     else:
         t.zero_()
@@ -200,7 +212,7 @@ def main():
     # ---------------- inputs (outside the timed region) ----------------
     halo = 64 if rank > 0 else 0
     blob = torch.empty(n + halo, dtype=torch.uint8, device="cuda")
-    make_blob(ctx, blob, rank * n - halo, n + halo, args.workload)
+    make_blob(ctx, blob, rank * n - halo, n + halo, args.workload, args.seed)
     d_ptr = blob.data_ptr() + halo
     cap = n // MIN + 4
     out = torch.empty(cap, dtype=torch.int64, device="cuda")
@@ -208,9 +220,10 @@ def main():
     lanes = []
     if world > 1:
         # N > 1: `inflight` pipeline lanes, each with its own library context
-        # and process group, run their share of the steps in host threads, so
-        # one lane's host round trips (seam record, RCCL all-gather, resolve)
-        # overlap another lane's kernels
+        # and process group; step s runs on lane s mod L.  A step is enqueued
+        # whole on its lane's stream (scan, stitch, seam record, RCCL
+        # all-gather, resolve, RCCL agreement) before the host waits for step
+        # s - L, the step's one host wait
         from desync_amd.shard import DeviceShard
         for i in range(max(1, args.inflight)):
             c_i = ctx if i == 0 else _lib.Context(gpu)
@@ -256,44 +269,20 @@ def main():
         return last
 
     def run_lanes(nsteps):
-        """N > 1: steps s = i, i + L, ... on lane i (one host thread each).  The
-        scans (dsx_shard_local) run concurrently; the exchange/resolve part of
-        each step runs in step order, so every rank issues its collectives in
-        the same order (no cross-communicator deadlock)."""
-        import threading
-
-        from desync_amd.shard import seam_protocol
-        res, errs = [None] * len(lanes), []
-        turn = {"next": 0}
-        cv = threading.Condition()
-
-        def lane(i):
-            try:
-                torch.cuda.set_device(gpu)  # (the current device is per thread)
-                for s in range(i, nsteps, len(lanes)):
-                    rec = lanes[i].local()
-                    with cv:
-                        cv.wait_for(lambda: turn["next"] == s or errs)
-                        if errs:
-                            return
-                        try:
-                            res[i] = seam_protocol(lanes[i], world, rec)
-                        finally:
-                            turn["next"] = s + 1
-                            cv.notify_all()
-            except BaseException as e:  # noqa: BLE001 -- re-raised below
-                with cv:
-                    errs.append(e)
-                    cv.notify_all()
-
-        ts = [threading.Thread(target=lane, args=(i,)) for i in range(len(lanes))]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        if errs:
-            raise errs[0]
-        return res[0]
+        """N > 1: step s on lane s mod L, from one host thread: every rank
+        issues the same collectives in the same order (no cross-communicator
+        deadlock), and up to L steps are queued on the GPU."""
+        from collections import deque
+        pending, last = deque(), None
+        for s in range(nsteps):
+            if len(pending) == len(lanes):
+                last = pending.popleft().finish()
+            ln = lanes[s % len(lanes)]
+            ln.begin()
+            pending.append(ln)
+        while pending:
+            last = pending.popleft().finish()
+        return last
 
     if world == 1:
         for s in range(args.warmup):
@@ -367,7 +356,7 @@ def main():
         dist.all_gather_object(lists, mine.tolist())
         if rank == 0:
             whole = torch.empty(n * world, dtype=torch.uint8, device="cuda")
-            make_blob(ctx, whole, 0, n * world, args.workload)
+            make_blob(ctx, whole, 0, n * world, args.workload, args.seed)
             ref = desync_amd.cut_device(whole.data_ptr(), n * world, MIN, AVG, MAX, ctx=ctx)
             got = np.array(sum(lists, []), dtype=np.uint64)
             assert np.array_equal(got, ref), "sharded cut list differs from the single-GPU one"
@@ -385,9 +374,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic ({DATA_LABEL[args.workload]}, generated on device)",
+            "data": f"synthetic ({DATA_LABEL[args.workload].format(seed=args.seed)}, generated on device)",
             "config": {
-                "workload": (f"{args.gib:g} GiB {args.workload} blob per GPU, desync make "
+                "workload": (f"{args.gib:g} GiB {args.workload} blob per GPU"
+                             f"{' (BASELINE config 5 shard shape)' if args.config5 else ''}, desync make "
                              f"min/avg/max 16/64/256 KiB, device-resident blob -> cut list in HBM"),
                 "bytes_per_gpu": n,
                 "chunks": int(chunks),

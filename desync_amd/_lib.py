@@ -44,6 +44,7 @@ DSX_SEAM_DEVICE = 8
 DSX_SEAM_LAST = 1
 DSX_SEAM_REWALKED = 2
 DSX_SEAM_ERROR = 4
+DSX_SEAM_REDO = 16
 
 # every symbol include/dsx.h declares (tests check the library exports them)
 EXPORTS = (
@@ -55,7 +56,8 @@ EXPORTS = (
     "dsx_stream_pop_many", "dsx_stream_window", "dsx_stream_unpop", "dsx_shard_local", "dsx_shard_resolve",
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host", "dsx_copy",
-    "dsx_ids_fd", "dsx_ids_host", "dsx_progress",
+    "dsx_ids_fd", "dsx_ids_host", "dsx_progress", "dsx_shard_resolve_async", "dsx_shard_collect",
+    "dsx_ctx_stream",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -164,6 +166,9 @@ def lib():
             "dsx_stream_chunk_data": (vp, [vp]),
             "dsx_shard_local": (i32, [vp, vp, u64, u64, u64, u64, P(Params), vp, u32]),
             "dsx_shard_resolve": (i32, [vp, vp, i32, i32, vp, vp, u64, P(u64), u32]),
+            "dsx_shard_resolve_async": (i32, [vp, vp, i32, i32, vp, u64, vp]),
+            "dsx_shard_collect": (i32, [vp, vp, vp, P(ctypes.c_int32), P(u64)]),
+            "dsx_ctx_stream": (i32, [vp, P(vp)]),
             "dsx_selftest_boundary": (i32, [vp, P(Params), i32, u64, u64, P(u64)]),
             "dsx_gen_uniform": (i32, [vp, vp, u64, u64, u64]),
             "dsx_gen_dedup": (i32, [vp, vp, u64, u64, u64, ctypes.c_double]),

@@ -31,7 +31,6 @@ static_assert(sizeof(dsx_seam_t) == 7 * 8 + 4 * 4 + 8 * (DSX_SEAM_MAX_CANDS + DS
 
 static void release_kept(dsx_ctx* c);
 
-constexpr uint64_t kSeamPeerFailed = 0x7FFFFFFFFFFFFFFFull;  // seam_resolve_kernel status
 
 int set_hip_err(dsx_ctx* c, hipError_t e, const char* what) {
   char buf[256];
@@ -184,6 +183,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     c->trace_keep = atoi(v) == 2;  // keep the traces of the last 4 pieces (slot = seq % 4)
   }
   if (const char* v = getenv("DSX_WAVE_MAJOR")) c->wave_major = atoi(v) != 0;
+  if (const char* v = getenv("DSX_SCAN_NT")) c->scan_nt = atoi(v) & 3;
   if (const char* v = getenv("DSX_FIXUP_FAST")) c->fixup_fast = atoi(v) != 0;
   if (const char* v = getenv("DSX_FINISH")) c->finish = atoi(v) != 0;
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
@@ -495,6 +495,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.queue = c->overflow.p + 32 + 256 * (seq % kQueueSlots);
   sa.queue_next = c->overflow.p + 32 + 256 * ((seq + 1) % kQueueSlots);
   sa.wave_major = c->wave_major ? 1u : 0u;
+  sa.nt_loads = (uint32_t)c->scan_nt;
   if (line) {
     // region 0's descriptor: the warm-up line unless it would start before
     // the readable bytes (then the 16-B step at or below base - min(halo, 48))
@@ -1062,7 +1063,13 @@ static void release_kept(dsx_ctx* c) {
 // re-walk (rewalk = true) only re-runs the stitch over the kept lists from
 // the new entry: O(candidates), no byte is read again.  (Pieces that needed
 // the dense-candidate path keep no lists; their re-walk scans again.)
-static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk) {
+// With async, nothing waits: the chain state is not read back (a stitch
+// error, including the overflow that the synchronous path retries on the
+// dense path, is published as DSX_SEAM_REDO in the record, see
+// seam_finalize_kernel) and sh.nspec stays unknown (the emit kernel reads the
+// count on the device).
+static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk,
+                     bool async = false) {
   auto& sh = c->sh;
   const dsx_params_t* p = &sh.p;
   const bool is_last = sh.start + sh.len == sh.total;
@@ -1127,6 +1134,10 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
                        (const uint64_t*)c->out.p, (const DevState*)c->state.p, sh.start, sh.len,
                        sh.total, wend0, entry, (is_last ? (uint32_t)DSX_SEAM_LAST : 0u) | rec_flags);
     HIPCHK(c, hipGetLastError());
+    if (async) {
+      sh.nspec = ~0ull;
+      return DSX_OK;
+    }
     HostState st;
     rc = read_state(c, &st);
     if (rc) return rc;
@@ -1146,11 +1157,12 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
   return DSX_E_INTERNAL;
 }
 
-// Copies the ctx's seam record to the caller's (host or device) record.
-static int seam_out(dsx_ctx* c, dsx_seam_t* seam, bool dev) {
+// Copies the ctx's seam record to the caller's (host or device) record; a
+// device record is left in flight on the ctx stream when `wait` is false.
+static int seam_out(dsx_ctx* c, dsx_seam_t* seam, bool dev, bool wait = true) {
   HIPCHK(c, hipMemcpyAsync(seam, c->d_seam.p, sizeof(dsx_seam_t),
                            dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (wait || !dev) HIPCHK(c, hipStreamSynchronize(c->stream));
   return DSX_OK;
 }
 
@@ -1158,8 +1170,10 @@ extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
                                uint64_t shard_start, uint64_t shard_len, uint64_t total,
                                const dsx_params_t* p, dsx_seam_t* seam, uint32_t flags) {
   if (!c || !p || !seam || (shard_len && !d_shard) || shard_start + shard_len > total ||
-      (flags & ~DSX_SEAM_DEVICE) != 0)
+      (flags & ~(DSX_SEAM_DEVICE | DSX_NO_SYNC)) != 0 ||
+      ((flags & DSX_NO_SYNC) && !(flags & DSX_SEAM_DEVICE)))
     return DSX_E_INVAL;
+  const bool async = (flags & DSX_NO_SYNC) != 0;
   if (shard_start > 0 && halo < kRound) return DSX_E_INVAL;
   c->cancel.store(0);
   int rc = ensure_attr_walk(c);
@@ -1185,10 +1199,62 @@ extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
     sh.valid = true;
     return seam_out(c, seam, (flags & DSX_SEAM_DEVICE) != 0);
   }
-  rc = shard_run(c, shard_start, 0u, false);
+  rc = shard_run(c, shard_start, 0u, false, async);
   if (rc) return rc;
   sh.valid = true;
-  return seam_out(c, seam, (flags & DSX_SEAM_DEVICE) != 0);
+  return seam_out(c, seam, (flags & DSX_SEAM_DEVICE) != 0, !async);
+}
+
+// The resolve outcome published by shard_emit_kernel (h_res), interpreted on
+// the host: DSX_OK with the count, DSX_E_PEER, or DSX_E_RESYNC after this
+// rank re-walked (a seam that did not converge) or redid (DSX_SEAM_REDO) its
+// shard and rewrote `my_seam`.  A failed re-walk / redo marks `my_seam`
+// DSX_SEAM_ERROR and returns its error.
+static int shard_outcome(dsx_ctx* c, int rank, dsx_seam_t* my_seam, bool seam_dev, uint64_t cap,
+                         uint64_t* n_out) {
+  const uint64_t status = c->h_res[0], n = c->h_res[1], entry = c->h_res[2];
+  *n_out = 0;
+  if (status == ~0ull) {
+    c->err = "shard: resolve did not publish its result";
+    return DSX_E_INTERNAL;
+  }
+  if (status == kSeamPeerFailed) return DSX_E_PEER;
+  if (status != 0) {
+    // kSeamRedo: rank `entry` redoes its shard from its own start; otherwise
+    // seam `status - 1` did not converge inside its window and its owner
+    // re-walks its shard from the true entry cut; either way the owner
+    // republishes its record
+    const bool redo = status == kSeamRedo;
+    const int failing = redo ? (int)entry : (int)(status - 1);
+    if (failing == rank) {
+      auto& sh = c->sh;
+      int rc = redo ? shard_run(c, sh.start, 0u, false) : shard_run(c, entry, DSX_SEAM_REWALKED, true);
+      if (rc) {
+        // publish the failure in this rank's record: the peers' next resolve
+        // returns DSX_E_PEER (ADVICE r1: no rank waits for a record forever)
+        const size_t off = offsetof(dsx_seam_t, flags);
+        uint32_t fl = 0;
+        const hipMemcpyKind d2h = seam_dev ? hipMemcpyDeviceToHost : hipMemcpyHostToHost;
+        const hipMemcpyKind h2d = seam_dev ? hipMemcpyHostToDevice : hipMemcpyHostToHost;
+        (void)hipStreamSynchronize(c->stream);
+        if (hipMemcpy(&fl, (const uint8_t*)my_seam + off, 4, d2h) == hipSuccess) {
+          fl |= DSX_SEAM_ERROR;
+          (void)hipMemcpy((uint8_t*)my_seam + off, &fl, 4, h2d);
+        }
+        return rc;
+      }
+      if (redo)
+        c->stats.dense_fallbacks++;
+      else
+        c->stats.repaired_segments++;
+      rc = seam_out(c, my_seam, seam_dev);
+      if (rc) return rc;
+    }
+    return DSX_E_RESYNC;
+  }
+  *n_out = n;
+  if (n > cap) return DSX_E_CAPACITY;
+  return DSX_OK;
 }
 
 extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks, int rank,
@@ -1213,7 +1279,7 @@ extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks
   hipLaunchKernelGGL(seam_resolve_kernel, dim3(1), dim3(64), 0, c->stream, d_all, nranks, rank,
                      sh.p.min, sh.p.max, c->d_ext.p, c->d_info.p);
   HIPCHK(c, hipGetLastError());
-  const uint64_t most = sh.nspec + DSX_SEAM_MAX_CUTS;
+  const uint64_t most = (sh.nspec == ~0ull ? sh.len / sh.p.min + 4 : sh.nspec) + DSX_SEAM_MAX_CUTS;
   uint64_t* dst = out_ends;
   uint64_t dcap = cap;
   if (!out_dev) {
@@ -1225,48 +1291,74 @@ extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks
   c->h_res[0] = ~0ull;
   hipLaunchKernelGGL(shard_emit_kernel, dim3(blocks), dim3(256), 0, c->stream,
                      (const uint64_t*)c->d_info.p, (const uint64_t*)c->d_ext.p,
-                     (const uint64_t*)c->out.p, sh.nspec, dst, dcap, (volatile uint64_t*)c->h_res);
+                     (const uint64_t*)c->out.p, (const DevState*)c->state.p, dst, dcap,
+                     (volatile uint64_t*)c->h_res, (int32_t*)nullptr);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint64_t status = c->h_res[0], n = c->h_res[1], entry = c->h_res[2];
-  if (status == ~0ull) {
-    c->err = "shard: resolve did not publish its result";
-    return DSX_E_INTERNAL;
-  }
-  if (status == kSeamPeerFailed) {
-    *n_out = 0;
-    return DSX_E_PEER;
-  }
-  if (status != 0) {
-    // seam `status - 1` did not converge inside its window: its owner re-walks
-    // its shard from the true entry cut and republishes its record
-    *n_out = 0;
-    const int failing = (int)(status - 1);
-    if (failing == rank) {
-      int rc = shard_run(c, entry, DSX_SEAM_REWALKED, true);
-      if (rc) {
-        // publish the failure in this rank's record: the peers' next resolve
-        // returns DSX_E_PEER (ADVICE r1: no rank waits for a record forever)
-        const size_t off = offsetof(dsx_seam_t, flags);
-        uint32_t fl = 0;
-        const hipMemcpyKind d2h = seam_dev ? hipMemcpyDeviceToHost : hipMemcpyHostToHost;
-        const hipMemcpyKind h2d = seam_dev ? hipMemcpyHostToDevice : hipMemcpyHostToHost;
-        (void)hipStreamSynchronize(c->stream);
-        if (hipMemcpy(&fl, (const uint8_t*)my_seam + off, 4, d2h) == hipSuccess) {
-          fl |= DSX_SEAM_ERROR;
-          (void)hipMemcpy((uint8_t*)my_seam + off, &fl, 4, h2d);
-        }
-        return rc;
-      }
-      c->stats.repaired_segments++;
-      rc = seam_out(c, my_seam, seam_dev);
-      if (rc) return rc;
-    }
-    return DSX_E_RESYNC;
-  }
-  *n_out = n;
-  if (n > cap) return DSX_E_CAPACITY;
+  int rc = shard_outcome(c, rank, my_seam, seam_dev, cap, n_out);
+  if (rc) return rc;
+  const uint64_t n = *n_out;
   if (!out_dev && n)
     HIPCHK(c, hipMemcpy(out_ends, c->d_emit.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return DSX_OK;
+}
+
+extern "C" int dsx_shard_resolve_async(dsx_ctx_t* c, const dsx_seam_t* all, int nranks, int rank,
+                                       uint64_t* out_ends, uint64_t cap, int32_t* d_code) {
+  if (!c || !all || nranks < 1 || rank < 0 || rank >= nranks || !out_ends || !d_code)
+    return DSX_E_INVAL;
+  auto& sh = c->sh;
+  if (!sh.valid) return DSX_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, grow(c, c->d_ext, DSX_SEAM_MAX_CUTS + 4));
+  HIPCHK(c, grow(c, c->d_info, 8));
+  hipLaunchKernelGGL(seam_resolve_kernel, dim3(1), dim3(64), 0, c->stream, all, nranks, rank,
+                     sh.p.min, sh.p.max, c->d_ext.p, c->d_info.p);
+  HIPCHK(c, hipGetLastError());
+  const uint64_t most = sh.len / sh.p.min + 4 + DSX_SEAM_MAX_CUTS;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((std::min(most, cap) + 255) / 256 + 1, 4096);
+  c->h_res[0] = ~0ull;
+  hipLaunchKernelGGL(shard_emit_kernel, dim3(blocks), dim3(256), 0, c->stream,
+                     (const uint64_t*)c->d_info.p, (const uint64_t*)c->d_ext.p,
+                     (const uint64_t*)c->out.p, (const DevState*)c->state.p, out_ends, cap,
+                     (volatile uint64_t*)c->h_res, d_code);
+  HIPCHK(c, hipGetLastError());
+  sh.pend_rank = rank;
+  sh.pend_cap = cap;
+  sh.pending = true;
+  return DSX_OK;
+}
+
+extern "C" int dsx_shard_collect(dsx_ctx_t* c, dsx_seam_t* my_seam, const int32_t* d_agreed,
+                                 int32_t* agreed, uint64_t* n_out) {
+  if (!c || !my_seam || !n_out || (d_agreed && !agreed)) return DSX_E_INVAL;
+  auto& sh = c->sh;
+  if (!sh.pending) return DSX_E_STATE;
+  sh.pending = false;
+  HIPCHK(c, hipSetDevice(c->device));
+  int32_t* h_code = (int32_t*)(c->h_res + 3);
+  if (d_agreed)
+    HIPCHK(c, hipMemcpyAsync(h_code, d_agreed, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the step's one host wait
+  if (d_agreed) *agreed = *h_code;
+  if (d_agreed && *h_code >= 2) {
+    // a rank failed this round: report this rank's own failure if it has one
+    const uint64_t status = c->h_res[0], n = c->h_res[1];
+    *n_out = 0;
+    if (status == ~0ull) return DSX_E_INTERNAL;
+    if (status == 0 && n > sh.pend_cap) {
+      *n_out = n;
+      return DSX_E_CAPACITY;
+    }
+    return DSX_E_PEER;
+  }
+  int rc = shard_outcome(c, sh.pend_rank, my_seam, true, sh.pend_cap, n_out);
+  if (rc == DSX_OK) c->stats.chunks = *n_out;
+  return rc;
+}
+
+extern "C" int dsx_ctx_stream(dsx_ctx_t* c, void** stream) {
+  if (!c || !stream) return DSX_E_INVAL;
+  *stream = (void*)c->stream;
   return DSX_OK;
 }

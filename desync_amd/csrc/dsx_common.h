@@ -71,6 +71,7 @@ struct ScanArgs {
   uint32_t shift0;
   uint64_t* trace;       // diagnostics (DSX_SCAN_TRACE): per wave slot {start, end, regions}
   uint32_t wave_major;   // first regions wave-major over the grid (DSX_WAVE_MAJOR, default 1)
+  uint32_t nt_loads;     // line DMA cache policy 0..3 (DSX_SCAN_NT, see dma16x8)
   uint32_t pad_;
 };
 

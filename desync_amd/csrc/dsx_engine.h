@@ -45,7 +45,9 @@ __global__ void seam_finalize_kernel(dsx_seam_t* seam, const uint64_t* cuts, con
 __global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
                                     uint64_t max, uint64_t* ext, uint64_t* info);
 __global__ void shard_emit_kernel(const uint64_t* info, const uint64_t* ext, const uint64_t* spec,
-                                  uint64_t nspec, uint64_t* out, uint64_t cap, volatile uint64_t* res);
+                                  const DevState* st, uint64_t* out, uint64_t cap,
+                                  volatile uint64_t* res, int32_t* code);
+
 }  // namespace dsx
 
 using namespace dsx;
@@ -127,6 +129,7 @@ struct dsx_ctx {
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
   bool wave_major = true;             // DSX_WAVE_MAJOR: scanl's first regions wave-major
+  int scan_nt = 1;                    // DSX_SCAN_NT: line DMA cache policy (0 none, 1 nt: default, 2 sc1, 3 sc0 sc1 nt)
   bool finish = true;                 // DSX_FINISH=0: fixup_fast_kernel + gather_kernel instead of finish_kernel
   bool fixup_fast = true;             // DSX_FIXUP_FAST=0: fixup_kernel for every piece
   DevBuf<uint64_t> trace;       // [4 * trace_n scan records][10 * trace_walk_n walk records]
@@ -206,7 +209,10 @@ struct dsx_ctx {
     const uint8_t* d = nullptr;  // caller's shard bytes (valid until resolve returns OK)
     uint64_t halo = 0, start = 0, len = 0, total = 0;
     dsx_params_t p{};
-    uint64_t nspec = 0;  // speculative cuts in ctx->out
+    uint64_t nspec = 0;  // speculative cuts in ctx->out (~0: unknown, asynchronous local)
+    bool pending = false;              // dsx_shard_resolve_async awaits dsx_shard_collect
+    int pend_rank = 0;
+    uint64_t pend_cap = 0;
     bool valid = false;
     bool dense = false;                // scanned on the dense path (lists not kept)
     std::vector<KeptPiece> kept;       // the shard's pieces' region lists

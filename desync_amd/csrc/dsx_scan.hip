@@ -71,42 +71,55 @@ __device__ __forceinline__ void dma16(const u32x4& rsrc, uint32_t voff, uint32_t
 // One line batch of scanl_kernel: 8 LDS-DMA wave instructions into 8
 // consecutive 1 KiB LDS blocks from lds_base, M0 saved once and stepped by
 // 1 KiB (per-instruction dma16 calls saved and restored M0 around each one:
-// 8 issue slots per instruction instead of 4).
+// 8 issue slots per instruction instead of 4).  POL selects the cache policy
+// of the loads: 0 default, 1 nt (streamed), 2 sc1, 3 sc0 sc1 nt (DSX_SCAN_NT).
+#define DSX_DMA8(POLSTR)                                                              \
+  asm volatile("s_mov_b32 %0, m0\n\t"                                                 \
+               "s_mov_b32 m0, %9\n\t"                                                 \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %1, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_add_u32 m0, m0, 0x400\n\t"                                          \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %2, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_add_u32 m0, m0, 0x400\n\t"                                          \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %3, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_add_u32 m0, m0, 0x400\n\t"                                          \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %4, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_add_u32 m0, m0, 0x400\n\t"                                          \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %5, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_add_u32 m0, m0, 0x400\n\t"                                          \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %6, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_add_u32 m0, m0, 0x400\n\t"                                          \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %7, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_add_u32 m0, m0, 0x400\n\t"                                          \
+               "s_nop 0\n\t"                                                          \
+               "buffer_load_dwordx4 %8, %10, 0 offen " POLSTR "lds\n\t"               \
+               "s_mov_b32 m0, %0"                                                       \
+               : "=&s"(keep)                                                            \
+               : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), \
+                 "v"(vo[6]), "v"(vo[7]), "s"(lds_base), "s"(rsrc)                       \
+               : "memory", "scc")
+
+template <int POL = 0>
 __device__ __forceinline__ void dma16x8(const u32x4& rsrc, const uint32_t (&vo)[8],
                                         uint32_t lds_base) {
   uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %9\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %10, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %10, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %3, %10, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %4, %10, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %5, %10, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %6, %10, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %7, %10, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %8, %10, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), "v"(vo[6]),
-        "v"(vo[7]), "s"(lds_base), "s"(rsrc)
-      : "memory", "scc");
+  if constexpr (POL == 1) {
+    DSX_DMA8("nt ");
+  } else if constexpr (POL == 2) {
+    DSX_DMA8("sc1 ");
+  } else if constexpr (POL == 3) {
+    DSX_DMA8("sc0 sc1 nt ");
+  } else {
+    DSX_DMA8("");
+  }
 }
+#undef DSX_DMA8
 
 // L2 prefetch: one dword per lane (buffer_load_dword ... lds) into the first
 // 256 B of a staging slot that the next DMA overwrites (loads retire in issue
@@ -686,7 +699,12 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       asm volatile("" : "+s"(ssum));
       vo[i] = (b < NB) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
     }
-    dma16x8(rsrc, vo, stage_lds);
+    switch (a.nt_loads) {
+      case 1: dma16x8<1>(rsrc, vo, stage_lds); break;
+      case 2: dma16x8<2>(rsrc, vo, stage_lds); break;
+      case 3: dma16x8<3>(rsrc, vo, stage_lds); break;
+      default: dma16x8<0>(rsrc, vo, stage_lds); break;
+    }
   };
 
   // wave-major first regions: when regions do not fill every wave slot, the

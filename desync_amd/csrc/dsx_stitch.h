@@ -65,6 +65,8 @@ struct HostState {
 };
 constexpr uint32_t kErrCapacity = 1u;  // output capacity exceeded
 constexpr uint32_t kErrDense = 2u;     // a lane overflowed its candidate slots
+constexpr uint64_t kSeamPeerFailed = 0x7FFFFFFFFFFFFFFFull;  // seam_resolve_kernel statuses
+constexpr uint64_t kSeamRedo = 0x7FFFFFFFFFFFFFFEull;
 
 constexpr uint32_t kMaxSpg = 255;  // segments per walk workgroup (+1 redundant)
 

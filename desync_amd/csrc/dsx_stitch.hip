@@ -223,7 +223,6 @@ __device__ __forceinline__ uint64_t seg_end(const StitchArgs& a, uint32_t k) {
 }
 
 // ---- K2: per-segment speculative walks ------------------------------------
-constexpr int kWalkThreads = 256;
 constexpr uint32_t kWalkMaxRegions = 4096;  // regions a walk workgroup can stage
 
 // Block-wide exclusive scan of one value per thread (NT threads); returns the
@@ -1078,7 +1077,11 @@ __global__ void seam_finalize_kernel(dsx_seam_t* seam, const uint64_t* cuts, con
   seam->entry = entry;
   seam->ncands = ncand;
   seam->ncuts = nc;
-  seam->flags = flags;
+  // an asynchronous dsx_shard_local does not read the chain state back: a
+  // stitch error (e.g. a lane that overflowed its candidate slots, which the
+  // synchronous path retries on the dense path) is published in the record,
+  // and every rank's resolve asks the owner to redo its shard synchronously
+  seam->flags = flags | (st->err ? (uint32_t)DSX_SEAM_REDO : 0u);
   seam->pad = 0;
 }
 
@@ -1102,13 +1105,23 @@ struct SeamSrc {
 // info: [0] 0, or 1 + the first rank whose seam did not converge; [1] c_rank
 // (keep the speculative cuts >= c_rank), or on failure the true entry cut of
 // the failing rank; [2] number of cuts written to ext (the true cuts of
-// `rank` before c_rank).
+// `rank` before c_rank).  A record flagged DSX_SEAM_ERROR gives
+// [0] = kSeamPeerFailed, one flagged DSX_SEAM_REDO [0] = kSeamRedo, [1] = its
+// rank.
 __global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank, uint64_t min,
                                     uint64_t max, uint64_t* ext, uint64_t* info) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   for (int r = 0; r < nranks; ++r) {
     if (all[r].flags & DSX_SEAM_ERROR) {  // a peer failed: every rank stops
-      info[0] = 0x7FFFFFFFFFFFFFFFull;
+      info[0] = kSeamPeerFailed;
+      info[1] = (uint64_t)r;
+      info[2] = 0;
+      return;
+    }
+  }
+  for (int r = 0; r < nranks; ++r) {
+    if (all[r].flags & DSX_SEAM_REDO) {  // rank r redoes its shard, then everyone resyncs
+      info[0] = kSeamRedo;
       info[1] = (uint64_t)r;
       info[2] = 0;
       return;
@@ -1161,23 +1174,27 @@ __global__ void seam_resolve_kernel(const dsx_seam_t* all, int nranks, int rank,
   info[2] = mine_n;
 }
 
-// This rank's final cut list = ext cuts, then the speculative cuts >= c_rank;
-// the count and status go to pinned host memory (res[0] status, [1] count,
-// [2] entry of the failing rank).
+// This rank's final cut list = ext cuts, then the speculative cuts >= c_rank
+// (the st->total cuts the shard's chain left in `spec`); the count and status
+// go to pinned host memory (res[0] status, [1] count, [2] entry of the failing
+// rank), and the round's outcome to `code` (device, may be null) for the
+// ranks' device-side agreement: 0 done, 1 exchange again, 2 failed.
 __global__ __launch_bounds__(256) void shard_emit_kernel(const uint64_t* info, const uint64_t* ext,
-                                                         const uint64_t* spec, uint64_t nspec,
+                                                         const uint64_t* spec, const DevState* st,
                                                          uint64_t* out, uint64_t cap,
-                                                         volatile uint64_t* res) {
+                                                         volatile uint64_t* res, int32_t* code) {
   const uint64_t status = info[0];
   if (status != 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       res[0] = status;
       res[1] = 0;
       res[2] = info[1];
+      if (code) *code = status == kSeamPeerFailed ? 2 : 1;
       __threadfence_system();
     }
     return;
   }
+  const uint64_t nspec = st->total;
   const uint64_t cr = info[1], next = info[2];
   uint64_t lo = 0, hi = nspec;  // first spec cut >= cr
   while (lo < hi) {
@@ -1194,6 +1211,7 @@ __global__ __launch_bounds__(256) void shard_emit_kernel(const uint64_t* info, c
     res[0] = 0;
     res[1] = n;
     res[2] = 0;
+    if (code) *code = n <= cap ? 0 : 2;
     __threadfence_system();
   }
 }

@@ -22,10 +22,13 @@ first cut starts in an earlier shard, at most max bytes back; the ranks
 all-gather the tails behind their last cut (the "overlap bytes" of the seams,
 <= max each), and each rank hashes its chunks on its own GPU.
 
-The protocol loop (seam_protocol) is shared by every transport: host records
-over any torch.distributed backend (shard_chunk), HBM records over RCCL
-(DeviceShard, bench.py), and the gloo CPU test, which plugs the oracle's
-restatement of the two library calls into the same loop.
+Two forms of the protocol loop, each shared by its transports and driven on
+the CPU by the gloo tests with the oracle's restatement of the library calls:
+seam_protocol (synchronous calls, host records over any torch.distributed
+backend: shard_chunk) and device_protocol (dsx_shard_resolve_async /
+dsx_shard_collect, records in HBM: DeviceShard, bench.py), which over RCCL
+keeps the whole step on the library stream -- one host wait per converged
+step.
 """
 from __future__ import annotations
 
@@ -34,7 +37,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import DSX_E_PEER, DSX_E_RESYNC, DSX_OUT_DEVICE, DSX_SEAM_DEVICE, check, lib
+from ._lib import DSX_E_PEER, DSX_E_RESYNC, DSX_NO_SYNC, DSX_SEAM_DEVICE, check, lib
 
 SEAM_BYTES = ctypes.sizeof(_lib.Seam)
 FLAGS_OFF = _lib.Seam.flags.offset
@@ -192,11 +195,106 @@ def shard_chunk(d_ptr, halo, shard_start, shard_len, total, params, ctx=None, gr
     return seam_protocol(eng, eng.world)
 
 
+def device_protocol(engine, world):
+    """The asynchronous form of seam_protocol (dsx_shard_resolve_async /
+    dsx_shard_collect), as a generator: it yields once, when the step's work
+    is enqueued and the next thing would be the host's wait, and returns this
+    rank's result (StopIteration.value; see run_device_protocol).  A
+    pipelined caller starts step k+1 between the two.
+
+    engine: local_async() enqueues the shard's scan + stitch + seam record;
+    mark_error() replaces the record with a DSX_SEAM_ERROR one; gather()
+    all-gathers the records; resolve() enqueues the resolve, whose round
+    outcome (AGREE_*) lands in a device word; collect() waits and returns
+    ("ok" | "resync" | "peer", agreed) or raises this rank's failure; result().
+    With engine.device_agree (RCCL) the ranks agree on the device before the
+    wait: fail_code() overwrites the word with AGREE_FAIL and reduce() enqueues
+    its MAX all-reduce, so a converged step waits on the host exactly once
+    (in collect).  Without it (records staged through host memory, e.g. gloo)
+    the agreement is agree() after collect, as in seam_protocol.
+
+    A failure before this rank's code is known (local_async / resolve) is published
+    in the same round (its record or its code says FAIL); one found by collect
+    after a device agreement (a failed re-walk, which marks the record
+    DSX_SEAM_ERROR) is published by one more exchange round.  Either way every
+    rank raises in the same round: nobody waits in a collective a peer left."""
+    err = None
+    try:
+        engine.local_async()
+    except BaseException as e:  # noqa: BLE001 -- raised once the peers know
+        err = e
+        engine.mark_error()
+    if not engine.device_agree:
+        yield
+    for rnd in range(world + 1):
+        engine.gather()
+        if err is None:
+            try:
+                engine.resolve()
+            except BaseException as e:  # noqa: BLE001
+                err = e
+        if engine.device_agree:
+            if err is not None:
+                engine.fail_code()
+            engine.reduce()
+            if err is not None:
+                raise err
+            if rnd == 0:
+                yield
+            try:
+                out, agreed = engine.collect()
+            except BaseException as e:  # noqa: BLE001 -- published next round
+                err = e
+                continue
+        else:
+            out = None
+            if err is None:
+                try:
+                    out, _ = engine.collect()
+                except BaseException as e:  # noqa: BLE001
+                    err = e
+            code = (AGREE_FAIL if err is not None or out == "peer" else
+                    AGREE_RESYNC if out == "resync" else AGREE_OK)
+            agreed = engine.agree(code)
+            if err is not None:
+                raise err
+        if agreed == AGREE_FAIL or out == "peer":
+            raise PeerFailed("a peer rank failed during seam resolution")
+        if agreed == AGREE_OK:
+            return engine.result()
+    if err is not None:
+        raise err
+    raise RuntimeError("seam resolution did not settle within nranks rounds")
+
+
+def _drive(g):
+    """Runs a device_protocol generator to its end; returns its result."""
+    while True:
+        try:
+            next(g)
+        except StopIteration as stop:
+            return stop.value
+
+
+def run_device_protocol(engine, world):
+    return _drive(device_protocol(engine, world))
+
+
+_COLLECT_RC = {0: "ok", DSX_E_RESYNC: "resync", DSX_E_PEER: "peer"}
+
+
 class DeviceShard:
-    """The N>1 path with the seam records in HBM (RCCL all-gather in place).
+    """The N>1 path with the seam records in HBM (bench.py's step).
 
     ``run()`` chunks this rank's shard and returns its exact cut count; the
-    cuts stay in ``self.out`` (an int64 device tensor) -- the bench's step.
+    cuts stay in ``self.out`` (an int64 device tensor).  Everything is
+    ordered on the library context's stream (``dsx_ctx_stream``, wrapped as a
+    torch ExternalStream): the asynchronous dsx_shard_local, the RCCL
+    all-gather of the 16 KiB records, dsx_shard_resolve_async and the RCCL
+    MAX all-reduce of the round code -- one host wait per converged step
+    (dsx_shard_collect).  ``begin()`` / ``finish()`` split a step at that wait
+    for a pipelined caller.  Over gloo (CPU tensors) the records are staged
+    through host memory and the ranks agree on the host: two waits.
     """
 
     def __init__(self, ctx, d_ptr, halo, shard_start, shard_len, total, params, group=None):
@@ -207,64 +305,91 @@ class DeviceShard:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.nccl = dist.get_backend(group) == "nccl"
+        self.device_agree = dist.get_backend(group) == "nccl"
         dev = torch.device("cuda", ctx.device)
         self.seam = torch.empty(SEAM_BYTES, dtype=torch.uint8, device=dev)
         self.all = torch.empty(self.world * SEAM_BYTES, dtype=torch.uint8, device=dev)
         self.cap = shard_len // params.min + 4 + _lib.DSX_SEAM_MAX_CUTS
         self.out = torch.empty(self.cap, dtype=torch.int64, device=dev)
+        self.code = torch.zeros(1, dtype=torch.int32, device=dev)
         self.n = ctypes.c_uint64()
+        self.agreed = ctypes.c_int32()
+        sp = ctypes.c_void_p()
+        check(lib().dsx_ctx_stream(ctx.h, ctypes.byref(sp)), ctx.h)
+        self.stream = torch.cuda.ExternalStream(sp.value, device=dev)
+        self._g = None
 
-    # -- engine interface (seam_protocol) --------------------------------------
-    def local(self):
+    # -- engine interface (device_protocol) ------------------------------------
+    def local_async(self):
         L, h = lib(), self.ctx.h
         check(L.dsx_shard_local(h, ctypes.c_void_p(self.d_ptr), self.halo, self.start, self.len,
                                 self.total, ctypes.byref(self.params.c),
-                                ctypes.c_void_p(self.seam.data_ptr()), DSX_SEAM_DEVICE), h)
-        return self.seam
+                                ctypes.c_void_p(self.seam.data_ptr()),
+                                DSX_SEAM_DEVICE | DSX_NO_SYNC), h)
 
-    def exchange(self, rec):
+    def mark_error(self):
+        import torch
+        with torch.cuda.stream(self.stream):
+            self.seam.zero_()
+            self.seam[FLAGS_OFF] = _lib.DSX_SEAM_ERROR
+
+    def gather(self):
         import torch
         import torch.distributed as dist
-        if self.nccl:
-            dist.all_gather_into_tensor(self.all, rec, group=self.group)
-        else:  # e.g. gloo (CPU tensors only): stage through host memory
-            mine = rec.cpu()
-            bufs = [torch.empty_like(mine) for _ in range(self.world)]
-            dist.all_gather(bufs, mine, group=self.group)
-            self.all.copy_(torch.cat(bufs))
-        torch.cuda.current_stream().synchronize()
-        return self.all
+        with torch.cuda.stream(self.stream):
+            if self.device_agree:
+                dist.all_gather_into_tensor(self.all, self.seam, group=self.group)
+            else:  # e.g. gloo (CPU tensors only): stage through host memory
+                mine = self.seam.cpu()
+                bufs = [torch.empty_like(mine) for _ in range(self.world)]
+                dist.all_gather(bufs, mine, group=self.group)
+                self.all.copy_(torch.cat(bufs))
 
-    def failed(self, allrec):
-        # the records stay in HBM: dsx_shard_resolve checks their flags on the
-        # device and returns DSX_E_PEER (no host round trip per step)
-        return []
+    def resolve(self):
+        check(lib().dsx_shard_resolve_async(self.ctx.h, ctypes.c_void_p(self.all.data_ptr()),
+                                            self.world, self.rank,
+                                            ctypes.c_void_p(self.out.data_ptr()), self.cap,
+                                            ctypes.c_void_p(self.code.data_ptr())), self.ctx.h)
+
+    def fail_code(self):
+        import torch
+        with torch.cuda.stream(self.stream):
+            self.code.fill_(AGREE_FAIL)
+
+    def reduce(self):
+        import torch
+        import torch.distributed as dist
+        with torch.cuda.stream(self.stream):
+            dist.all_reduce(self.code, op=dist.ReduceOp.MAX, group=self.group)
+
+    def collect(self):
+        d_agreed = ctypes.c_void_p(self.code.data_ptr()) if self.device_agree else None
+        rc = lib().dsx_shard_collect(self.ctx.h, ctypes.c_void_p(self.seam.data_ptr()), d_agreed,
+                                     ctypes.byref(self.agreed), ctypes.byref(self.n))
+        if rc not in _COLLECT_RC:
+            check(rc, self.ctx.h)
+        return _COLLECT_RC[rc], (self.agreed.value if self.device_agree else None)
 
     def agree(self, code):
-        import torch
-        return agree_max(code, self.group, torch.device("cuda", self.ctx.device) if self.nccl else None)
-
-    def resolve(self, allrec):
-        rc = lib().dsx_shard_resolve(self.ctx.h, ctypes.c_void_p(allrec.data_ptr()), self.world,
-                                     self.rank, ctypes.c_void_p(self.seam.data_ptr()),
-                                     ctypes.c_void_p(self.out.data_ptr()), self.cap,
-                                     ctypes.byref(self.n), DSX_SEAM_DEVICE | DSX_OUT_DEVICE)
-        return _resolve_rc(rc, self.ctx.h)
-
-    def record(self):
-        return self.seam
-
-    def mark_error(self, rec):
-        rec[FLAGS_OFF] = int(rec[FLAGS_OFF].item()) | _lib.DSX_SEAM_ERROR
-        return rec
+        return agree_max(code, self.group)
 
     def result(self):
         return self.n.value
 
     # -- bench step ------------------------------------------------------------
+    def begin(self):
+        """Enqueue a step (up to the host wait)."""
+        self._g = device_protocol(self, self.world)
+        next(self._g)
+
+    def finish(self):
+        """Complete the step begun last; returns the exact cut count."""
+        g, self._g = self._g, None
+        return _drive(g)
+
     def run(self):
-        return seam_protocol(self, self.world)
+        self.begin()
+        return self.finish()
 
     def cuts(self):
         return self.out[:self.n.value].cpu().numpy().astype(np.uint64)

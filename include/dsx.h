@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSX_ABI_VERSION 3
+#define DSX_ABI_VERSION 4
 
 /* ---- error codes (negative) ---------------------------------------------- */
 enum {
@@ -234,6 +234,8 @@ const uint8_t *dsx_stream_chunk_id(dsx_ctx_t *ctx);
 #define DSX_SEAM_LAST 1u        /* seam flags: the shard ends the blob */
 #define DSX_SEAM_REWALKED 2u    /* seam flags: chain re-walked from the true entry `entry` */
 #define DSX_SEAM_ERROR 4u       /* seam flags: the owner failed; every rank's resolve returns DSX_E_PEER */
+#define DSX_SEAM_REDO 16u       /* seam flags: an asynchronous dsx_shard_local hit a stitch error; the
+                                   owner redoes its shard synchronously (dsx_shard_collect) */
 typedef struct dsx_seam {
     uint64_t shard_start, shard_len, total;
     uint64_t first_cand_beyond;   /* first candidate > window end, or UINT64_MAX */
@@ -251,6 +253,35 @@ int dsx_shard_local(dsx_ctx_t *ctx, const void *d_shard, uint64_t halo, uint64_t
 int dsx_shard_resolve(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, int rank,
                       dsx_seam_t *my_seam, uint64_t *out_ends, uint64_t cap, uint64_t *n_out,
                       uint32_t flags);
+
+/* Asynchronous step (device records, device cut list): at most one host wait
+ * per converged step.
+ *   dsx_shard_local(..., DSX_SEAM_DEVICE | DSX_NO_SYNC) enqueues the scan,
+ *     stitch and record on the ctx stream and returns (a stitch error shows up
+ *     as DSX_SEAM_REDO in the record instead of a return code);
+ *   the caller all-gathers the records on the ctx stream (dsx_ctx_stream);
+ *   dsx_shard_resolve_async enqueues the resolve: this rank's final cuts go to
+ *     out_ends (device, cap entries) and the round's outcome to the device
+ *     int32 *d_code: 0 done, 1 exchange again, 2 failed (a peer's
+ *     DSX_SEAM_ERROR, or cap too small);
+ *   the caller all-reduces the code words with MAX on the ctx stream (the
+ *     ranks' agreement, so a local failure reaches every rank in this round);
+ *   dsx_shard_collect waits once, copies the agreed word (d_agreed, device,
+ *     or NULL when the caller agrees on the host) to *agreed and returns what
+ *     dsx_shard_resolve would: DSX_OK with *n_out, DSX_E_RESYNC (the owner of
+ *     a non-converged or DSX_SEAM_REDO seam has re-walked / redone its shard
+ *     and rewritten my_seam, device memory), DSX_E_PEER, or an error (then
+ *     my_seam is marked DSX_SEAM_ERROR when the failure happened after the
+ *     agreement: exchange once more so the peers learn of it).  With an
+ *     agreed code of 2 it returns this rank's own failure (DSX_E_CAPACITY) or
+ *     DSX_E_PEER. */
+int dsx_shard_resolve_async(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, int rank,
+                            uint64_t *out_ends, uint64_t cap, int32_t *d_code);
+int dsx_shard_collect(dsx_ctx_t *ctx, dsx_seam_t *my_seam, const int32_t *d_agreed,
+                      int32_t *agreed, uint64_t *n_out);
+/* The ctx's HIP stream (hipStream_t), for ordering a caller's collectives
+ * with the library's kernels without host waits. */
+int dsx_ctx_stream(dsx_ctx_t *ctx, void **stream);
 
 /* Synchronous copy of n bytes between any host / device pointers (hipMemcpy
  * with the direction inferred): a binding without its own GPU runtime uses it

@@ -23,9 +23,16 @@ def test_cpu_share_reads_omp_num_threads(monkeypatch):
     assert 1 <= bench.cpu_share() <= 16
 
 
-def test_data_labels_name_the_generator_seeds():
-    assert "seed 1" in bench.DATA_LABEL["uniform"]
-    assert "seed 2" in bench.DATA_LABEL["dedup"]
+def test_data_labels_name_the_generator_seeds(monkeypatch):
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    a = bench.parse()
+    assert "seed 1" in bench.DATA_LABEL["uniform"].format(seed=a.seed)
+    monkeypatch.setattr("sys.argv", ["bench.py", "--workload", "dedup"])
+    a = bench.parse()
+    assert "seed 2" in bench.DATA_LABEL["dedup"].format(seed=a.seed)
+    monkeypatch.setattr("sys.argv", ["bench.py", "--config5"])
+    a = bench.parse()
+    assert (a.gib, a.seed, a.workload) == (32.0, 3, "uniform")  # BASELINE config 5's shards
 
 
 def test_cpu_leg_matches_the_sequential_chain():

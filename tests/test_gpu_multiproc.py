@@ -8,6 +8,10 @@ over "gloo" (RCCL needs one GPU per rank; the seam protocol is the same).
   zero run across the seam that forces the O(candidates) re-walk.
 * bench.py's DeviceShard path (records in HBM) under torch.distributed.run
   with --check, as the driver launches it for N > 1.
+* DeviceShard over RCCL (the driver's N > 1 backend) in a one-rank "nccl"
+  group -- RCCL needs one GPU per rank, so this is the only RCCL shape a
+  one-GPU box can run: the asynchronous step with the all-gather and the
+  agreement all-reduce on the library stream, pipelined over two lanes.
 """
 import hashlib
 import os
@@ -114,3 +118,50 @@ def test_bench_two_ranks_gloo_check():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "check ok" in r.stderr, r.stderr[-2000:]
     assert '"n_gpus": 2' in r.stdout
+
+
+def _nccl_worker(port, q):
+    sys.path.insert(0, REPO)
+    import torch
+    import torch.distributed as dist
+
+    import desync_amd
+    from desync_amd import _lib
+    from desync_amd.shard import DeviceShard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from oracle import oracle as o
+        n = (64 << 20) + 4321
+        host = o.synth_uniform(61, 0, n)
+        t = torch.from_numpy(host).to("cuda:0")
+        p = desync_amd.Params(MIN, AVG, MAX)
+        ctxs = [_lib.Context(0), _lib.Context(0)]
+        lanes = [DeviceShard(ctxs[0], t.data_ptr(), 0, 0, n, n, p),
+                 DeviceShard(ctxs[1], t.data_ptr(), 0, 0, n, n, p, group=dist.new_group())]
+        assert all(ln.device_agree for ln in lanes)
+        counts = []
+        for s in range(6):  # step s on lane s % 2, one step queued ahead
+            lanes[s % 2].begin()
+            if s:
+                counts.append(lanes[(s - 1) % 2].finish())
+        counts.append(lanes[1].finish())
+        ref = o.chunk_stream(host, MIN, AVG, MAX)
+        q.put((counts, [ln.cuts().tolist() == ref.tolist() for ln in lanes], int(ref.size)))
+        for c in ctxs:
+            c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_device_shard_rccl_one_rank():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    proc = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    proc.start()
+    counts, same, nref = q.get(timeout=240)
+    proc.join(timeout=60)
+    assert proc.exitcode == 0
+    assert counts == [nref] * 6 and all(same)

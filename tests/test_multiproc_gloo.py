@@ -99,6 +99,71 @@ class OracleEngine:
         return self.mine
 
 
+class OracleDeviceEngine(OracleEngine):
+    """device_protocol's engine interface over the same CPU restatement, with
+    the library's asynchronous semantics: resolve() only computes the round
+    code (the device word), reduce() is the ranks' MAX agreement on it (RCCL
+    on the GPU; gloo here), and collect() applies the outcome afterwards
+    (the owner's re-walk).  With device_agree False the agreement comes after
+    collect, as over host-staged records.  ``fail`` injects a failure in
+    start, resolve or the re-walk."""
+
+    def __init__(self, data, rank, world, fail=None, device_agree=True):
+        super().__init__(data, rank, world)
+        self.fail, self.device_agree = fail, device_agree
+        self.recb = None
+
+    def local_async(self):
+        if self.fail == "start":
+            raise IOError("injected failure")
+        self.recb = self.local()
+
+    def mark_error(self):
+        from desync_amd import _lib
+        S = _lib.Seam()
+        S.flags = _lib.DSX_SEAM_ERROR
+        self.recb = self.sh.seam_to_bytes(S)
+
+    def gather(self):
+        self.allb = self.sh.exchange_seams(self.recb)
+
+    def resolve(self):
+        from oracle import seam as oseam
+        self.rounds += 1
+        if self.fail == "resolve":
+            raise IOError("injected failure")
+        if self.sh.failed_ranks(self.allb, self.world):
+            self.pend, self.code = ("peer",), 2
+            return
+        seams = [_from_struct(s) for s in self.sh.seams_from_bytes(self.allb, self.world)]
+        self.pend = oseam.resolve(seams, self.rank, MIN, MAX)
+        self.code = 0 if self.pend[0] == "ok" else 1
+
+    def fail_code(self):
+        self.code = 2
+
+    def reduce(self):
+        self.agreed = self.sh.agree_max(self.code)
+
+    def collect(self):
+        from oracle import seam as oseam
+        agreed = self.agreed if self.device_agree else None
+        if agreed == 2 or self.pend[0] == "peer":
+            return "peer", agreed
+        st, a, b = self.pend
+        if st == "ok":
+            self.mine = oseam.rank_cuts(a, b, self.spec)
+            return "ok", agreed
+        if a == self.rank:
+            if self.fail == "rewalk":
+                self.mark_error()  # as dsx_shard_collect marks my_seam
+                raise IOError("injected failure")
+            self.rec, self.spec = oseam.rewalk(self.cands, b, self.start, self.length,
+                                               self.data.size, MIN, MAX)
+            self.recb = self.record()
+        return "resync", agreed
+
+
 def _worker(rank, world, port, data, result_q, fail_rank):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -170,5 +235,72 @@ def test_seam_protocol_failure_propagates(world, fail_rank, kind):
     which raises PeerFailed; nobody hangs.  "random" data settles in round 1
     (the peers' own resolves say "ok"), "seam-zero-run" needs re-walks."""
     msgs = _run(_compose(kind), world, fail_rank)
+    kinds = sorted((m[1], m[0]) for m in msgs)
+    assert kinds == [(r, "own" if r == fail_rank else "peer") for r in range(world)]
+
+
+def _dworker(rank, world, port, data, result_q, fail_rank, fail, device_agree):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    from desync_amd import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = OracleDeviceEngine(data, rank, world, fail if rank == fail_rank else None, device_agree)
+    try:
+        mine = shard.run_device_protocol(eng, world)
+        out = [None] * world
+        dist.all_gather_object(out, mine.tolist())
+        if rank == 0:
+            result_q.put(("ok", sum(out, []), eng.rounds))
+    except shard.PeerFailed:
+        result_q.put(("peer", rank, None))
+    except IOError:
+        result_q.put(("own", rank, None))
+    dist.destroy_process_group()
+
+
+def _drun(data, world, fail_rank=None, fail=None, device_agree=True):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dworker,
+                         args=(r, world, port, data, q, fail_rank, fail, device_agree))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(1 if fail_rank is None else world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return msgs
+
+
+@pytest.mark.parametrize("device_agree", [True, False])
+@pytest.mark.parametrize("kind,world", [("random", 2), ("seam-zero-run", 2), ("seam-zero-run", 3),
+                                        ("spread-null", 3)])
+def test_device_protocol_gloo(kind, world, device_agree):
+    """DeviceShard's asynchronous loop (one host wait per converged step)
+    gives the sequential chunker's cut list, re-walks included."""
+    from oracle import oracle as o
+    data = _compose(kind)
+    (st, got, rounds), = _drun(data, world, device_agree=device_agree)
+    assert st == "ok"
+    assert got == o.chunk_stream(data, MIN, AVG, MAX).tolist()
+    if kind == "seam-zero-run":
+        assert rounds > 1
+
+
+@pytest.mark.parametrize("device_agree", [True, False])
+@pytest.mark.parametrize("fail,world,fail_rank", [("start", 2, 0), ("start", 3, 2),
+                                                  ("resolve", 3, 1), ("rewalk", 2, 1),
+                                                  ("rewalk", 3, 1)])
+def test_device_protocol_failure_propagates(fail, world, fail_rank, device_agree):
+    """A rank failing before its round code is known (start, resolve) or after
+    the device agreement (its re-walk, on a zero run across every seam): the
+    failing rank raises its own error, every other rank PeerFailed, nobody
+    hangs."""
+    kind = "seam-zero-run" if fail == "rewalk" else "random"
+    msgs = _drun(_compose(kind), world, fail_rank, fail, device_agree)
     kinds = sorted((m[1], m[0]) for m in msgs)
     assert kinds == [(r, "own" if r == fail_rank else "peer") for r in range(world)]
