@@ -139,6 +139,11 @@ constexpr uint32_t kRelClamp = 0xFFFFFFF0u;
 struct RelChain {
   uint32_t min, max, L, PE;  // L, PE relative to lo, clamped to kRelClamp
   bool is_last;
+  // the same bounds folded for branch-free steps: a chain at s >= tail_at
+  // ends at L (chunker.go:215-217: len - s <= min); steps are capped at
+  // lim_cap (L: chunker.go:221); a bound beyond undet_at is undetermined
+  // (non-final piece).  Unused bounds are 0xFFFFFFFF.
+  uint32_t tail_at, lim_cap, undet_at, end_at;
 };
 __device__ __forceinline__ uint32_t rel_clamp(uint64_t v, uint64_t lo) {
   return v <= lo ? 0u : (v - lo >= kRelClamp ? kRelClamp : (uint32_t)(v - lo));
@@ -153,20 +158,22 @@ __device__ __forceinline__ RelChain rel_chain(const ChainParams& w, uint64_t lo)
   r.L = rel_clamp(w.L, lo);
   r.PE = rel_clamp(w.PE, lo);
   r.is_last = w.is_last != 0;
+  r.tail_at = r.is_last ? (r.L > r.min ? r.L - r.min : 0u) : 0xFFFFFFFFu;
+  r.lim_cap = r.is_last ? r.L : 0xFFFFFFFFu;
+  r.undet_at = r.is_last ? 0xFFFFFFFFu : r.PE;
+  r.end_at = r.is_last ? r.L : 0xFFFFFFFFu;
   return r;
 }
 // next(s) of chunker.go:206-277 for a relative chain position s (< L when
-// is_last); kRelUndet if the successor depends on bytes beyond the piece
+// is_last); kRelUndet if the successor depends on bytes beyond the piece.
+// Straight-line scalar code around one ballot step (the walks are
+// latency-bound: every branch and wait is on the chain's critical path).
 __device__ __forceinline__ uint32_t rel_next(uint32_t s, WaveLdsSrc& src, const RelChain& w) {
-  uint32_t lim = s + w.max;
-  if (w.is_last) {
-    if (w.L - s <= w.min) return w.L;  // chunker.go:215-217
-    if (lim > w.L) lim = w.L;          // chunker.go:221
-  }
+  if (s >= w.tail_at) return w.L;                  // chunker.go:215-217
+  const uint32_t lim = min(s + w.max, w.lim_cap);  // chunker.go:221
   const uint32_t c = src.next_after32(s + w.min);  // chunker.go:259-271
   if (c <= lim) return c;                          // (none = 0xFFFFFFFF > lim)
-  if (!w.is_last && lim > w.PE) return kRelUndet;
-  return lim;  // chunker.go:276
+  return lim > w.undet_at ? kRelUndet : lim;       // chunker.go:276
 }
 
 // Candidates straight from the scan's per-region sorted lists (global
@@ -351,6 +358,10 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   constexpr uint32_t kWaves = kWalkThreads / 64;
   // ---- phase 1: speculative chain of each segment -> exit X_k (one wave each) ----
+  // A chain step is a ballot over the 64 candidates the wave holds in a
+  // register, s_ff1 and a readlane; the chain's cuts go into one register
+  // (lane i = cut i) and to LDS once at the end, so no step
+  // waits on LDS (each step's LDS store used to cost an lgkmcnt(0) wait)
   if (!dense) {
     for (uint32_t t = wv; t < nwalk; t += kWaves) {
       const uint32_t k = kFirst + t;
@@ -361,24 +372,25 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
       if (tr && t == wv) tr[7] = __builtin_amdgcn_s_memrealtime();
       const uint32_t er = rel_clamp(e, lo);
       uint32_t x = rel_clamp(v, lo), last = x;
-      uint32_t steps = 0, ns = 0, why = 0;
-      uint32_t* spec = s_spec + t * a.scap;
+      uint32_t ns = 0, why = 0;
+      uint32_t specv = 0;  // lane i: the chain's i-th cut (i < 64)
       while (true) {
-        if (rc.is_last && x >= rc.L) { why = 1; break; }
+        if (x >= rc.end_at) { why = 1; break; }
         const uint32_t nx = rel_next(x, src, rc);
-        if (tr && t == wv && steps == 0) tr[8] = __builtin_amdgcn_s_memrealtime();
-        ++steps;
         if (nx == kRelUndet) { why = 2; break; }
         if (nx > er) break;
-        if (record && ln == 0 && ns < a.scap) spec[ns] = nx;
+        specv = ln == ns ? nx : specv;  // (v_cmp + v_cndmask; no lane >= 64)
         ++ns;
         last = nx;
         x = nx;
       }
       if (tr && t == wv) tr[9] = __builtin_amdgcn_s_memrealtime();
+      // (more than 64 cuts, or more than the LDS holds: no phase-2 shortcut)
+      const bool keep = record && ns <= 64u && ns <= a.scap;
+      if (keep && ln < ns) s_spec[t * a.scap + ln] = specv;
       if (ln == 0) {
         xs[t] = lo + last;
-        s_spec_n[t] = ns <= a.scap ? ns : 0xFFFFFFFFu;  // overflow: no shortcut
+        s_spec_n[t] = keep ? ns : 0xFFFFFFFFu;
         s_spec_end[t] = why;
         if (k >= kA) a.seg_info[k].X = lo + last;  // kA-1 belongs to the previous workgroup
       }
@@ -417,12 +429,12 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
     uint32_t n = 0, flags = 0;
     const uint32_t er = rel_clamp(e, lo), sr = rel_clamp(sst, lo);
     uint32_t x = rel_clamp(E, lo), last = x;
-    // the speculative chain of this segment (phase 1), if recorded
+    // the speculative chain of this segment (phase 1), one cut per lane
     const uint32_t sn = record ? s_spec_n[t] : 0xFFFFFFFFu;
-    const uint32_t* spec = s_spec + t * a.scap;
-    uint32_t sp = 0;  // first spec cut not below the staged chain
+    const bool have_spec = sn != 0xFFFFFFFFu;
+    const uint32_t specv = have_spec && ln < sn ? s_spec[t * a.scap + ln] : 0xFFFFFFFFu;
     while (true) {
-      if (rc.is_last && x >= rc.L) { flags |= kSegEnd; break; }
+      if (x >= rc.end_at) { flags |= kSegEnd; break; }
       const uint32_t nx = rel_next(x, src, rc);
       if (nx == kRelUndet) { flags |= kSegUndet; break; }
       if (nx > er) break;
@@ -432,16 +444,16 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
       }
       last = nx;
       x = nx;
-      if (sn != 0xFFFFFFFFu) {
-        while (sp < sn && spec[sp] < nx) ++sp;
-        if (sp < sn && spec[sp] == nx) {
+      if (have_spec) {
+        const uint64_t hit = __ballot(specv == nx);
+        if (hit) {
           // met the speculative chain (all its cuts are > sst): the staged
           // chain continues with its cuts and ends the way it ended
-          const uint32_t rest = sn - sp - 1;
-          for (uint32_t q = ln; q < rest; q += 64)
-            if (n + q < a.scap) out[n + q] = lo + spec[sp + 1 + q];
+          const uint32_t f = (uint32_t)__builtin_ctzll(hit);
+          const uint32_t rest = sn - f - 1;
+          if (ln > f && ln < sn && n + (ln - f - 1) < a.scap) out[n + (ln - f - 1)] = lo + specv;
           n += rest;
-          if (rest) last = spec[sn - 1];
+          if (rest) last = (uint32_t)__builtin_amdgcn_readlane((int)specv, (int)(sn - 1));
           if (s_spec_end[t] == 1) flags |= kSegEnd;
           if (s_spec_end[t] == 2) flags |= kSegUndet;
           break;

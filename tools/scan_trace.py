@@ -93,6 +93,5 @@ if len(wk):
     print(f"walk workgroups {len(wk)} (times from the first scan wave start, us)")
     for i, name in enumerate(["entry", "counts", "staged", "walk1", "walk2"]):
         print(f"  {name:7s} pct {q} {np.percentile(rel[:, i], q).round(1).tolist()}")
-    sub = (wk[:, 7:10] - t0) / 100.0
-    for i, name in enumerate(["seek", "step1", "chain"]):
-        print(f"  {name:7s} pct {q} {np.percentile(sub[:, i], q).round(1).tolist()}")
+    for c, name in ((7, "seek"), (9, "chain")):
+        print(f"  {name:7s} pct {q} {np.percentile((wk[:, c] - t0) / 100.0, q).round(1).tolist()}")
