@@ -854,6 +854,23 @@ __global__ __launch_bounds__(kFinThreads) void finish_kernel(StitchArgs a) {
       fl[j] = si.flags;
     }
   }
+  // this workgroup's segments' staged lists (wave wv takes kb + wv + 4q), loaded
+  // now so that their round trip overlaps the SegInfo loads instead of
+  // following the count scan (the stage buffer holds nseg * scap entries)
+  constexpr int QW = (int)kFinSegPerWg / (NT / 64);
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  const uint32_t kb = blockIdx.x * kFinSegPerWg;
+  const uint32_t ke = kb + kFinSegPerWg < T ? kb + kFinSegPerWg : T;
+  uint64_t v[QW];
+  {
+    const uint32_t sc1 = a.scap - 1;
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      uint32_t k = kb + wv + (uint32_t)q * (NT / 64);
+      k = k < T ? k : T - 1;
+      v[q] = a.stage[(uint64_t)k * a.scap + (lane < sc1 ? lane : sc1)];
+    }
+  }
   const bool last_wg = blockIdx.x == gridDim.x - 1;
   if (skip) {  // what fixup_kernel publishes when the piece was not walked
     if (last_wg && tid == 0) {
@@ -910,7 +927,6 @@ __global__ __launch_bounds__(kFinThreads) void finish_kernel(StitchArgs a) {
       my_last = Z[j];
     }
   }
-  const uint32_t lane = tid & 63, wv = tid >> 6;
   uint64_t incl = mine;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -946,19 +962,6 @@ __global__ __launch_bounds__(kFinThreads) void finish_kernel(StitchArgs a) {
   const uint64_t piece = s_piece;
   const bool fits = base + piece <= a.out_cap;
   if (fits) {
-    // this workgroup's segments, wave wv takes kb + wv + 4q: the loads of
-    // its segments are issued together (one memory round trip)
-    constexpr int QW = (int)kFinSegPerWg / (NT / 64);
-    const uint32_t kb = blockIdx.x * kFinSegPerWg;
-    const uint32_t ke = kb + kFinSegPerWg < T ? kb + kFinSegPerWg : T;
-    const uint32_t sc1 = a.scap - 1;
-    uint64_t v[QW];
-#pragma unroll
-    for (int q = 0; q < QW; ++q) {
-      uint32_t k = kb + wv + (uint32_t)q * (NT / 64);
-      k = k < T ? k : T - 1;
-      v[q] = a.stage[(uint64_t)k * a.scap + (lane < sc1 ? lane : sc1)];
-    }
 #pragma unroll
     for (int q = 0; q < QW; ++q) {
       const uint32_t k = kb + wv + (uint32_t)q * (NT / 64);
