@@ -55,10 +55,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the cpu_baseline leg (0: the job's CPU share)")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="chunking jobs kept in flight (one library context each), so the "
-                         "host's wait for job k overlaps the GPU work of job k+1 (N > 1: "
-                         "pipeline lanes, one library context and process group each)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="chunking jobs kept in flight (0: 4 at N = 1, queued on one library "
+                         "context; N > 1: 3 pipeline lanes, one library context and process "
+                         "group each)")
     ap.add_argument("--check", action="store_true",
                     help="N>1: compare the concatenated per-rank cut lists with one "
                          "dsx_cut_device over the whole blob on rank 0 (small sizes)")
@@ -67,6 +67,8 @@ def parse():
         args.gib, args.workload, args.seed = 32.0, "uniform", 3
     if not args.seed:
         args.seed = 2 if args.workload == "dedup" else 1
+    if args.inflight <= 0:
+        args.inflight = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
     return args
 
 
@@ -235,8 +237,10 @@ def main():
     # list in HBM) whose count the host collects.  Up to `inflight` jobs are
     # queued on the context (DSX_NO_SYNC): job s is enqueued before the host
     # waits for job s - inflight, so the GPU is not idle while the host wakes
-    # up, and the library runs job s's stitch beside job s+1's scan (its scans
-    # own a CU-masked stream).
+    # up.  Each job's stitch follows its scan on the library stream; the host
+    # polls the state the stitch publishes (no event between jobs).  With
+    # DSX_FUSE=1 a queued job's stitch runs as tasks inside the next two jobs'
+    # scans instead (throughput-neutral under the power cap).
     depth = min(8, max(1, args.inflight)) if world == 1 else 1
     outs = [torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(depth)]
     queued = []

@@ -186,6 +186,8 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SCAN_NT")) c->scan_nt = atoi(v) & 3;
   if (const char* v = getenv("DSX_FIXUP_FAST")) c->fixup_fast = atoi(v) != 0;
   if (const char* v = getenv("DSX_FINISH")) c->finish = atoi(v) != 0;
+  if (const char* v = getenv("DSX_FUSE")) c->fuse = atoi(v) != 0;
+
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_LANE_TARGET"))
@@ -228,12 +230,14 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     }
   }
   CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
-  CREATE_STEP(hipHostMalloc((void**)&c->h_ring, kQueueDepth * sizeof(HostState)));
+  // coherent: dsx_result polls the seq the GPU publishes here
+  CREATE_STEP(hipHostMalloc((void**)&c->h_ring, kQueueDepth * sizeof(HostState), hipHostMallocCoherent));
   memset(c->h_ring, 0, kQueueDepth * sizeof(HostState));
   c->h_cur = c->h_state;
   for (uint32_t i = 0; i < kQueueDepth; ++i)
     CREATE_STEP(hipEventCreateWithFlags(&c->q_ev[i], hipEventDisableTiming));
   CREATE_STEP(hipHostMalloc((void**)&c->h_res, 4 * sizeof(uint64_t)));
+  CREATE_STEP(hipHostMalloc((void**)&c->h_tasks, dsx_ctx::kTaskRing * sizeof(TaskArgs), hipHostMallocCoherent));
   memset(c->h_state, 0, sizeof(HostState));
   CREATE_STEP(c->state.ensure(1));
   // [0..1] overflow (piece parity); [32 + 256*parity + 32*x] the scan's work
@@ -257,10 +261,12 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
   c->dg_ends.release(); c->dg_ids.release(); c->dg_queue.release();
   c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
+  c->seg_info2.release(); c->stage2.release(); c->spec.release(); c->spec2.release();
   release_kept(c);
   c->zero_word.release();
   c->d_seam.release(); c->d_all.release(); c->d_ext.release(); c->d_info.release(); c->d_emit.release();
   if (c->h_res) (void)hipHostFree(c->h_res);
+  if (c->h_tasks) (void)hipHostFree(c->h_tasks);
   index_release(c);
   stream_release(c);
   if (c->h_state) (void)hipHostFree(c->h_state);
@@ -312,6 +318,7 @@ extern "C" int dsx_progress(dsx_ctx_t* c, uint64_t* bytes) {
 
 extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64_t* n_scan,
                                uint64_t* n_walk) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !n_scan || !n_walk) return DSX_E_INVAL;
   *n_scan = c->trace_n;
   *n_walk = c->trace_walk_n;
@@ -326,6 +333,7 @@ extern "C" int dsx_debug_trace(dsx_ctx_t* c, uint64_t* out, uint64_t cap, uint64
 }
 
 extern "C" int dsx_copy(dsx_ctx_t* c, void* dst, const void* src, uint64_t n) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || (n && (!dst || !src))) return DSX_E_INVAL;
   if (!n) return DSX_OK;
   HIPCHK(c, hipSetDevice(c->device));
@@ -458,7 +466,9 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   } else {
     // split streams: two region-list sets, so the next piece's scan writes
     // one while this piece's stitch reads the other
-    const bool second = split && (c->piece_seq + 1) % 2 == 1;
+    // (and stitch behind: the next scan writes one while its tasks walk
+    // the other)
+    const bool second = (split || cc.behind) && (c->piece_seq + 1) % 2 == 1;
     auto& bc = second ? c->region_cnt2 : c->region_cnt;
     auto& bl = second ? c->region_list2 : c->region_list;
     HIPCHK(c, grow(c, bc, nregions));
@@ -468,6 +478,63 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   }
   c->last_rcnt = rcnt;
   c->last_rlist = rlist;
+  // stitch behind: this call's segment set (by piece parity), and the tasks
+  // of the calls behind it that this scan carries
+  dsx_ctx::Behind me;
+  TaskArgs tb{};
+  if (cc.behind) {
+    const bool second = (c->piece_seq + 1) % 2 == 1;
+    const uint64_t seg = std::max<uint64_t>(c->seg_max_mult * p->max, c->seg_floor);
+    const uint64_t nseg = (len + seg - 1) / seg;
+    const uint32_t scap = (uint32_t)(seg / p->min + 3);
+    auto& bs = second ? c->seg_info2 : c->seg_info;
+    auto& bt = second ? c->stage2 : c->stage;
+    auto& bp = second ? c->spec2 : c->spec;
+    if (bs.n < nseg || bt.n < nseg * scap || bp.n < nseg * scap) {
+      // the call two back may still have to finish from this set: launch it
+      // on its own before the set is reallocated
+      int rc = flush_behind(c);
+      if (rc) return rc;
+      HIPCHK(c, grow(c, bs, nseg));
+      HIPCHK(c, grow(c, bt, nseg * scap));
+      HIPCHK(c, grow(c, bp, nseg * scap));
+    }
+    // segments per walk task (one lane each, up to 63): the task's
+    // candidates fill at most half of its LDS on average
+    const double exp_per_seg = (double)seg / (double)p->discriminator + 8.0;
+    me.wseg = (uint32_t)std::max(1.0, std::min(32.0, std::floor(kTaskCand / (2.0 * exp_per_seg)) - 1.0));
+    me.fseg = 32;
+    me.nw = (uint32_t)((nseg + me.wseg - 1) / me.wseg);
+    me.nf = (uint32_t)((nseg + me.fseg - 1) / me.fseg);
+    me.w.min = p->min;
+    me.w.max = p->max;
+    me.w.L = len;
+    me.w.seg = seg;
+    me.w.nseg = (uint32_t)nseg;
+    me.w.scap = scap;
+    me.w.seg_info = bs.p;
+    me.w.stage = bt.p;
+    me.w.spec = bp.p;
+    me.f.seg_info = bs.p;
+    me.f.stage = bt.p;
+    me.f.spec = bp.p;
+    me.f.nseg = (uint32_t)nseg;
+    me.f.scap = scap;
+    me.f.out = cc.d_out;
+    me.f.out_cap = cc.out_cap;
+    me.f.host_state = c->h_cur;
+    for (const auto& b : c->behind) {
+      if (!b.walked) {
+        tb.w = b.w;
+        tb.nw = b.nw;
+        tb.wseg = b.wseg;
+      } else {
+        tb.f = b.f;
+        tb.nf = b.nf;
+        tb.fseg = b.fseg;
+      }
+    }
+  }
   const uint64_t seq = ++c->piece_seq;
   const int par = (int)(seq & 1);
   hipStream_t ss = c->scan_stream;
@@ -494,8 +561,18 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.overflow_next = c->overflow.p + ((seq + 1) % kQueueSlots);
   sa.queue = c->overflow.p + 32 + 256 * (seq % kQueueSlots);
   sa.queue_next = c->overflow.p + 32 + 256 * ((seq + 1) % kQueueSlots);
-  sa.wave_major = c->wave_major ? 1u : 0u;
+  sa.wave_major = c->wave_major ? (cc.behind ? 2u : 1u) : 0u;
   sa.nt_loads = (uint32_t)c->scan_nt;
+  tb.counter = sa.queue + 1;  // (zeroed by the previous scan, with the queue)
+  tb.farrive = sa.queue + 2;
+
+  if (cc.behind) {
+    // the ring slot was last read by the scan kTaskRing pieces ago, which
+    // completed before any of the kQueueDepth queued calls still pending
+    TaskArgs* slot = c->h_tasks + (seq % dsx_ctx::kTaskRing);
+    *slot = tb;
+    sa.tasks = slot;
+  }
   if (line) {
     // region 0's descriptor: the warm-up line unless it would start before
     // the readable bytes (then the 16-B step at or below base - min(halo, 48))
@@ -511,8 +588,11 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     const uint64_t slot_words = kScanTraceWords * c->trace_n + 10 * 65536ull;
     HIPCHK(c, grow(c, c->trace, (c->trace_keep ? 4 : 1) * slot_words));
     c->trace_base = c->trace_keep ? (seq % 4) * slot_words : 0;
-    HIPCHK(c, hipMemsetAsync(c->trace.p + c->trace_base, 0, kScanTraceWords * c->trace_n * sizeof(uint64_t), ss));
+    // (stitch behind: 6 task words per wave slot follow, read as walk records)
+    const uint64_t tw = cc.behind ? 6 * c->trace_n : 0;
+    HIPCHK(c, hipMemsetAsync(c->trace.p + c->trace_base, 0, (kScanTraceWords * c->trace_n + tw) * sizeof(uint64_t), ss));
     sa.trace = c->trace.p + c->trace_base;
+    if (cc.behind) c->trace_walk_n = (tw + 9) / 10;
   }
   const uint32_t pi = c->npiece_call++;
   while (c->pev.size() < 3 * (size_t)(pi + 1)) {
@@ -525,7 +605,10 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi], ss));
   {
     const uint64_t need_wg = std::max<uint64_t>(1, (nregions + W - 1) / W);
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)ncu_scan);
+    // (stitch behind: every CU, so the wave slots beyond the regions -- spread
+    // over the grid by the wave-major order -- run the tasks from the start)
+    const uint32_t grid = cc.behind ? (uint32_t)ncu_scan
+                                    : (uint32_t)std::min<uint64_t>(need_wg, (uint64_t)ncu_scan);
     const dim3 g(grid), b(W * kWave);
     const int mode = pick_mode(c, p->discriminator);
 #if DSX_DIAG
@@ -534,8 +617,14 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__>), g, b, 0, ss, sa); \
   else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__>), g, b, 0, ss, sa); \
   else
+#define DSX_ABLATEL(K, ...)                                                                \
+  if (c->variant == 1) hipLaunchKernelGGL((K<2, 1, __VA_ARGS__, false>), g, b, 0, ss, sa); \
+  else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__, false>), g, b, 0, ss, sa); \
+  else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__, false>), g, b, 0, ss, sa); \
+  else
 #else
 #define DSX_ABLATE(K, ...)
+#define DSX_ABLATEL(K, ...)
 #endif
 #define DSX_LAUNCH(BR, NB, WV, SUB, PF)                                                    \
   do {                                                                                     \
@@ -549,26 +638,28 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   } while (0)
 #if DSX_DIAG
 #define DSX_TRACE_VARIANTS(WV, SUB, D)                                                    \
-  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D>), g, b, 0, ss, sa); \
+  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D, false>), g, b, 0, ss, sa); \
   else if (c->variant == 6 && mode == 2)                                                  \
-    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D>), g, b, 0, ss, sa);         \
+    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D, false>), g, b, 0, ss, sa);         \
   else
 #else
 #define DSX_TRACE_VARIANTS(WV, SUB, D)
 #endif
-#define DSX_LAUNCHL(WV, SUB, D)                                                           \
+#define DSX_LAUNCHL(WV, SUB, D, FU)                                                       \
   do {                                                                                    \
-    DSX_ABLATE(scanl_kernel, WV, SUB, D)                                                  \
-    DSX_TRACE_VARIANTS(WV, SUB, D)                                                        \
     if (mode == 2)                                                                        \
-      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D>), g, b, 0, ss, sa);       \
+      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D, FU>), g, b, 0, ss, sa); \
     else if (mode == 1)                                                                   \
-      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D>), g, b, 0, ss, sa);       \
+      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D, FU>), g, b, 0, ss, sa); \
     else                                                                                  \
-      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D>), g, b, 0, ss, sa);       \
+      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D, FU>), g, b, 0, ss, sa); \
   } while (0)
-    if (line) {
-      DSX_LAUNCHL(8, 8, 1);
+    if (line && cc.behind) {
+      DSX_LAUNCHL(8, 8, 1, true);
+    } else if (line) {
+      DSX_ABLATEL(scanl_kernel, 8, 8, 1)
+      DSX_TRACE_VARIANTS(8, 8, 1)
+      DSX_LAUNCHL(8, 8, 1, false);
     } else {
 #if DSX_DIAG
       switch (c->scan_cfg) {
@@ -589,6 +680,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
 #undef DSX_LAUNCH
 #undef DSX_LAUNCHL
 #undef DSX_ABLATE
+#undef DSX_ABLATEL
 #undef DSX_TRACE_VARIANTS
     HIPCHK(c, hipGetLastError());
   }
@@ -609,6 +701,27 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     kp->pc = pc;
     kp->P = P;
     kp->len = len;
+  }
+  if (cc.behind) {
+    // the call two back finished in this scan, the last one walked in it;
+    // this one waits for the next scan (or flush_behind)
+    me.w.pc = pc;
+    me.f.overflow = sa.overflow;
+    me.f.seq = seq;
+    me.seq = seq;
+    std::deque<dsx_ctx::Behind> next;
+    for (auto& b : c->behind)
+      if (!b.walked) {
+        b.walked = true;
+        next.push_back(b);
+      }
+    next.push_back(me);
+    c->behind.swap(next);
+    c->init_pending = false;
+    c->last_finish = false;
+    if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi + 2], c->stream));
+    c->stats.pieces++;
+    return DSX_OK;
   }
   int rc = launch_stitch(c, cc, pc, P, len, is_last, seq, line && c->scan_trace);
   if (rc) return rc;
@@ -675,7 +788,9 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   ta.seq = seq;
   ta.init = c->init_pending ? 1u : 0u;  // the call's first piece: walk_kernel resets the state
   ta.init_carry = c->init_carry;
+  ta.arrive = c->overflow.p + kArriveWord;
   c->init_pending = false;
+  c->last_finish = false;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
   if (trace && walk_grid <= 65536) {
     ta.trace = c->trace.p + c->trace_base + kScanTraceWords * c->trace_n;
@@ -694,6 +809,7 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
     else if (nseg <= 1024) hipLaunchKernelGGL(finish_kernel<4>, fg, dim3(256), 0, c->stream, ta);
     else hipLaunchKernelGGL(finish_kernel<8>, fg, dim3(256), 0, c->stream, ta);
     HIPCHK(c, hipGetLastError());
+    c->last_finish = true;  // its publisher arrives last: the host may poll the seq
     return DSX_OK;
   }
   if (c->fixup_fast && nseg <= 8 * 1024) {
@@ -739,6 +855,51 @@ int ensure_attr_walk(dsx_ctx* c) {
   return DSX_OK;
 }
 
+int flush_behind(dsx_ctx* c) {
+  if (c->behind.empty()) return DSX_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  // round 1: the walked call's finish and the other's walk (independent);
+  // round 2: the latter's finish
+  while (!c->behind.empty()) {
+    TaskArgs tb{};
+    tb.farrive = c->overflow.p + kArriveWord + 1;
+    for (const auto& b : c->behind) {
+      if (!b.walked) {
+        tb.w = b.w;
+        tb.nw = b.nw;
+        tb.wseg = b.wseg;
+      } else {
+        tb.f = b.f;
+        tb.nf = b.nf;
+        tb.fseg = b.fseg;
+      }
+    }
+    const uint32_t n = tb.nw + tb.nf;
+    if (n) {
+      hipLaunchKernelGGL(stitch_task_kernel, dim3((n + 3) / 4), dim3(256), 0, c->stream, tb);
+      HIPCHK(c, hipGetLastError());
+    }
+    std::deque<dsx_ctx::Behind> next;
+    for (auto& b : c->behind)
+      if (!b.walked) {
+        b.walked = true;
+        next.push_back(b);
+      }
+    c->behind.swap(next);
+  }
+  return DSX_OK;
+}
+
+// A queued cut_device call that can be stitched behind later scans: one
+// line-aligned piece from 0, a candidate density the walk tasks' LDS holds.
+static bool behind_ok(dsx_ctx* c, const void* d_blob, uint64_t len, const dsx_params_t* p) {
+  if (!c->fuse || !c->scan_line || c->stitch_cus > 0 || c->variant) return false;
+  if (len == 0 || len > kPieceMax || ((uintptr_t)d_blob & (kLine - 1)) != 0) return false;
+  const uint64_t seg = std::max<uint64_t>(c->seg_max_mult * p->max, c->seg_floor);
+  const double exp_per_seg = (double)seg / (double)p->discriminator + 8.0;
+  return 4.0 * exp_per_seg <= (double)kTaskCand;  // wseg >= 1 with room to spare
+}
+
 static int finish_call(dsx_ctx* c, uint64_t* n_out, uint64_t cap, bool* dense_retry) {
   HostState s;
   int rc = read_state(c, &s);
@@ -767,6 +928,8 @@ static int finish_call(dsx_ctx* c, uint64_t* n_out, uint64_t cap, bool* dense_re
 
 extern "C" int dsx_sync(dsx_ctx_t* c) {
   if (!c) return DSX_E_INVAL;
+  int rc = flush_behind(c);
+  if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return DSX_OK;
 }
@@ -780,15 +943,40 @@ extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
   const dsx_ctx::Pending q = c->pend.front();
   c->pend.pop_front();
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipEventSynchronize(q.done));
+  if (q.behind) {  // its stitch still waits for a later scan: run it now
+    for (const auto& b : c->behind)
+      if (b.seq == q.seq) {
+        const int rc = flush_behind(c);
+        if (rc) return rc;
+        break;
+      }
+  }
+  if (q.done) {
+    HIPCHK(c, hipEventSynchronize(q.done));
+  } else {
+    // poll the published seq; the stream going idle without it is an error
+    const volatile uint64_t* sp = &c->h_ring[q.slot].seq;
+    for (uint32_t spins = 1; *sp != q.seq; ++spins) {
+      if (spins % 4096u == 0) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e == hipSuccess) break;  // (seq checked below)
+        if (e != hipErrorNotReady) return set_hip_err(c, e, "hipStreamQuery");
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
   HostState s;
   memcpy(&s, (const void*)&c->h_ring[q.slot], sizeof(HostState));
   if (s.seq != q.seq) {
     c->err = "stale chain state (queued call did not complete)";
     return DSX_E_INTERNAL;
   }
-  if (s.err & kErrDense) {  // rare: redo on the dense-candidate path, synchronously
-    c->stats.dense_fallbacks++;
+  if (s.err & (kErrDense | kErrRedo)) {
+    // rare: redo synchronously (dense-candidate path, or the general stitch
+    // with fixup_kernel's repair when a behind-the-scan stitch met a suspect
+    // segment)
+    if (s.err & kErrDense) c->stats.dense_fallbacks++;
     dsx_params_t p = q.p;
     return dsx_cut_device(c, q.d_blob, q.len, &p, q.out, q.cap, n_out, DSX_OUT_DEVICE);
   }
@@ -803,7 +991,7 @@ extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
     stitch += b;
   }
   c->stats.scan_ms = scan;
-  c->stats.stitch_ms = stitch;
+  c->stats.stitch_ms = q.behind ? 0.0f : stitch;  // (inside later scans)
   *n_out = s.total;
   if ((s.err & kErrCapacity) || s.total > q.cap) return DSX_E_CAPACITY;
   return DSX_OK;
@@ -819,12 +1007,19 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
   if (len == 0) return DSX_OK;  // TestChunkerEmptyFile: no chunks
   const bool dev_out = (flags & DSX_OUT_DEVICE) != 0;
   const uint64_t need = len / p->min + 2;
-  if ((flags & DSX_NO_SYNC) && dev_out) {
+  const bool queued = (flags & DSX_NO_SYNC) && dev_out;
+  const bool fuse = queued && behind_ok(c, d_blob, len, p);
+  if (!fuse) {  // every other call starts after the stitches still behind
+    rc = flush_behind(c);
+    if (rc) return rc;
+  }
+  if (queued) {
     if (c->pend.size() >= kQueueDepth) {
       c->err = "too many queued DSX_NO_SYNC calls (collect them with dsx_result)";
       return DSX_E_STATE;
     }
     CallCfg cc{p, len, 0, kRound, out_ends, cap, false};
+    cc.behind = fuse;
     dsx_ctx::Pending q;
     q.d_blob = d_blob;
     q.len = len;
@@ -846,7 +1041,12 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
     c->timing = true;
     c->h_cur = c->h_state;
     if (rc) return rc;
-    HIPCHK(c, hipEventRecord(q.done, c->stream));
+    // an event record costs ~6 us of stream time between two jobs (rocprofv3
+    // kernel trace): when finish_kernel ended the call, its last workgroup
+    // publishes the state after every cut is written, and dsx_result polls it
+    q.behind = fuse;
+    if (fuse || (!timed && c->last_finish)) q.done = nullptr;
+    else HIPCHK(c, hipEventRecord(q.done, c->stream));
     q.seq = c->piece_seq;
     c->pend.push_back(q);
     return DSX_OK;
@@ -971,6 +1171,7 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
 extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uint64_t start,
                              const uint64_t* ends, uint64_t n, void* ids, uint32_t flags,
                              int algo) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || (n && (!d_blob || !ends || !ids)) || (algo != DSX_DIGEST_SHA512_256 &&
                                                    algo != DSX_DIGEST_SHA256))
     return DSX_E_INVAL;
@@ -1023,6 +1224,7 @@ extern "C" int dsx_chunk_ids(dsx_ctx_t* c, const void* d_blob, uint64_t len, uin
 // --------------------------------------------------------------------------
 extern "C" int dsx_selftest_boundary(dsx_ctx_t* c, const dsx_params_t* p, int mode, uint64_t h0,
                                      uint64_t n, uint64_t* mismatches) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !p || !mismatches) return DSX_E_INVAL;
   HIPCHK(c, hipSetDevice(c->device));
   if (mode < 0) mode = pick_mode(c, p->discriminator);
@@ -1169,6 +1371,7 @@ static int seam_out(dsx_ctx* c, dsx_seam_t* seam, bool dev, bool wait = true) {
 extern "C" int dsx_shard_local(dsx_ctx_t* c, const void* d_shard, uint64_t halo,
                                uint64_t shard_start, uint64_t shard_len, uint64_t total,
                                const dsx_params_t* p, dsx_seam_t* seam, uint32_t flags) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !p || !seam || (shard_len && !d_shard) || shard_start + shard_len > total ||
       (flags & ~(DSX_SEAM_DEVICE | DSX_NO_SYNC)) != 0 ||
       ((flags & DSX_NO_SYNC) && !(flags & DSX_SEAM_DEVICE)))
@@ -1260,6 +1463,7 @@ static int shard_outcome(dsx_ctx* c, int rank, dsx_seam_t* my_seam, bool seam_de
 extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks, int rank,
                                  dsx_seam_t* my_seam, uint64_t* out_ends, uint64_t cap,
                                  uint64_t* n_out, uint32_t flags) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !all || nranks < 1 || rank < 0 || rank >= nranks || !n_out || !my_seam ||
       (cap && !out_ends) || (flags & ~(DSX_SEAM_DEVICE | DSX_OUT_DEVICE)) != 0)
     return DSX_E_INVAL;
@@ -1305,6 +1509,7 @@ extern "C" int dsx_shard_resolve(dsx_ctx_t* c, const dsx_seam_t* all, int nranks
 
 extern "C" int dsx_shard_resolve_async(dsx_ctx_t* c, const dsx_seam_t* all, int nranks, int rank,
                                        uint64_t* out_ends, uint64_t cap, int32_t* d_code) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !all || nranks < 1 || rank < 0 || rank >= nranks || !out_ends || !d_code)
     return DSX_E_INVAL;
   auto& sh = c->sh;
@@ -1331,6 +1536,7 @@ extern "C" int dsx_shard_resolve_async(dsx_ctx_t* c, const dsx_seam_t* all, int 
 
 extern "C" int dsx_shard_collect(dsx_ctx_t* c, dsx_seam_t* my_seam, const int32_t* d_agreed,
                                  int32_t* agreed, uint64_t* n_out) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !my_seam || !n_out || (d_agreed && !agreed)) return DSX_E_INVAL;
   auto& sh = c->sh;
   if (!sh.pending) return DSX_E_STATE;
@@ -1358,6 +1564,7 @@ extern "C" int dsx_shard_collect(dsx_ctx_t* c, dsx_seam_t* my_seam, const int32_
 }
 
 extern "C" int dsx_ctx_stream(dsx_ctx_t* c, void** stream) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !stream) return DSX_E_INVAL;
   *stream = (void*)c->stream;
   return DSX_OK;

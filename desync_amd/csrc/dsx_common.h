@@ -43,6 +43,8 @@ struct TestConsts {
   uint32_t vmax1;  // MODE 2, scanl: vmax + 1 (candidate => t + 1 < vmax1; d >= 3 keeps it < 2^32)
 };
 
+struct TaskArgs;  // dsx_stitch.h
+
 struct ScanArgs {
   const uint8_t* base;   // device pointer of the piece's first byte
   uint64_t halo;         // readable bytes before base (0 only at blob start)
@@ -73,6 +75,9 @@ struct ScanArgs {
   uint32_t wave_major;   // first regions wave-major over the grid (DSX_WAVE_MAJOR, default 1)
   uint32_t nt_loads;     // line DMA cache policy 0..3 (DSX_SCAN_NT, see dma16x8)
   uint32_t pad_;
+  // scanl_kernel<FUSE>: the stitch tasks it carries, in pinned host memory
+  // (read once per task; by value they held ~90 more SGPRs through the scan)
+  const TaskArgs* tasks;
 };
 
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches
@@ -81,6 +86,7 @@ constexpr int kLine = 128;
 constexpr int kScanTraceWords = 6;  // per wave: start, end, info, entry, region-end cycles, region-start waits
 constexpr int kQueueSlots = 4;                  // overflow / queue slots (piece seq mod 4)
 constexpr int kQueueWords = 32 + kQueueSlots * 256;  // overflow words + 4 x 8 queue counters
+constexpr int kArriveWord = 16;                 // finish_kernel's arrival counter (word 16)
 constexpr uint32_t kLineLaneMax = 384u * 170u;  // 65280
 
 // Sentinel for "successor depends on bytes beyond the piece" (non-final piece).

@@ -22,8 +22,9 @@ template <class H>
 __global__ void digest_pc_kernel(DigestArgs a);
 template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ void scan_kernel(ScanArgs a);
-template <int MODE, int VARIANT, int W, int SUB, int D>
+template <int MODE, int VARIANT, int W, int SUB, int D, bool FUSE>
 __global__ void scanl_kernel(ScanArgs a);
+__global__ void stitch_task_kernel(TaskArgs b);
 template <int NT>
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
@@ -155,6 +156,24 @@ struct dsx_ctx {
   uint64_t last_region_bytes = 0;  // geometry of the last enqueued piece's region lists
   uint32_t last_nregions = 0, last_region_cap = 0;
   uint64_t init_carry = 0;
+  bool last_finish = false;  // the last stitch ended with finish_kernel (publishes last)
+  // stitch behind the scan (DSX_FUSE, default on): queued one-piece calls
+  // whose walk (walked = false) or finish (walked = true) runs as tasks in
+  // the next queued call's scan; flush_behind() launches them on their own
+  struct Behind {
+    WalkJob w;
+    FinishJob f;
+    uint32_t nw = 0, nf = 0, wseg = 1, fseg = 1;
+    bool walked = false;
+    uint64_t seq = 0;
+  };
+  std::deque<Behind> behind;
+  bool fuse = false;  // DSX_FUSE=1 (off: throughput-neutral under the board's power cap)
+  static constexpr uint32_t kTaskRing = 16;  // > the launches a queued call can be behind
+  TaskArgs* h_tasks = nullptr;               // pinned ring: the TaskArgs of fused scans
+  DevBuf<SegInfo> seg_info2;  // the second segment set (calls of odd piece seq)
+  DevBuf<uint64_t> stage2;
+  DevBuf<uint64_t> spec, spec2;  // stitch tasks' speculative chains (per set)
 
   // streaming state (Chunker.Next over an io.Reader)
   struct Stream {
@@ -237,7 +256,8 @@ struct dsx_ctx {
     uint64_t* out = nullptr;
     uint32_t slot = 0;
     uint64_t seq = 0;       // piece sequence number of the call's last piece
-    hipEvent_t done = nullptr;
+    hipEvent_t done = nullptr;  // recorded after the call (null: poll the published seq)
+    bool behind = false;        // stitched behind later scans (c->behind)
     uint32_t npiece = 0;    // DSX_TIMED: pieces whose events are in q_pev[slot]
   };
   std::vector<hipEvent_t> q_pev[kQueueDepth];  // DSX_TIMED queued calls' piece events
@@ -298,6 +318,7 @@ struct CallCfg {
   bool dense;        // dense-candidate path
   uint64_t halo0 = 0;  // readable bytes before the first piece (shards)
   std::vector<KeptPiece>* keep = nullptr;  // keep every piece's region lists here
+  bool behind = false;  // one queued piece from 0: stitch behind later scans
 };
 
 // engine entry points (dsx_api.cpp)
@@ -306,6 +327,16 @@ int read_state(dsx_ctx* c, HostState* out);
 int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_t halo,
                   uint64_t P, uint64_t len, bool is_last);
 int ensure_attr_walk(dsx_ctx* c);
+// launch the stitch tasks of the queued calls still behind (before any other
+// work on the context, and when such a call is collected)
+int flush_behind(dsx_ctx* c);
+#define DSX_FLUSH_BEHIND(c)                  \
+  do {                                       \
+    if (c) {                                 \
+      const int rc_fb_ = flush_behind(c);    \
+      if (rc_fb_) return rc_fb_;             \
+    }                                        \
+  } while (0)
 int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t P, uint64_t len,
                   bool is_last, uint64_t seq, bool trace);
 // digest_kernel on `stream` (null: the ctx stream) with queue counter `queue`

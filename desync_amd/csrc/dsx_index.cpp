@@ -467,6 +467,7 @@ static bool bad_algo(int algo) { return algo != DSX_DIGEST_SHA512_256 && algo !=
 extern "C" int dsx_index_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, const dsx_params_t* p,
                             int algo, uint64_t* out_ends, uint8_t* ids, uint64_t cap,
                             uint64_t* n_out) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !p || !n_out || fd < 0 || (cap && (!out_ends || !ids)) || bad_algo(algo))
     return DSX_E_INVAL;
   if (len == UINT64_MAX) {
@@ -486,6 +487,7 @@ extern "C" int dsx_index_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, co
 // the digests.
 extern "C" int dsx_cut_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, const dsx_params_t* p,
                           uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !p || !n_out || fd < 0 || (cap && !out_ends)) return DSX_E_INVAL;
   if (len == UINT64_MAX) {
     const off_t end = lseek(fd, 0, SEEK_END);
@@ -500,6 +502,7 @@ extern "C" int dsx_cut_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, cons
 
 extern "C" int dsx_cut_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, const dsx_params_t* p,
                             uint64_t* out_ends, uint64_t cap, uint64_t* n_out) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !p || !n_out || (len && !h_blob) || (cap && !out_ends)) return DSX_E_INVAL;
   MemSrc s{(const uint8_t*)h_blob};
   const int rc = run_index(c, p, -1, len, fill_mem, &s, out_ends, nullptr, cap, n_out);
@@ -510,6 +513,7 @@ extern "C" int dsx_cut_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, cons
 extern "C" int dsx_index_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, const dsx_params_t* p,
                               int algo, uint64_t* out_ends, uint8_t* ids, uint64_t cap,
                               uint64_t* n_out) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !p || !n_out || (len && !h_blob) || (cap && (!out_ends || !ids)) || bad_algo(algo))
     return DSX_E_INVAL;
   MemSrc s{(const uint8_t*)h_blob};
@@ -523,6 +527,7 @@ extern "C" int dsx_index_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, co
 // chunk.go:60-73).
 extern "C" int dsx_ids_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, uint64_t start,
                           const uint64_t* ends, uint64_t n, int algo, uint8_t* ids) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || fd < 0 || (n && (!ends || !ids)) || bad_algo(algo)) return DSX_E_INVAL;
   if (len == UINT64_MAX) {
     const off_t end = lseek(fd, 0, SEEK_END);
@@ -537,6 +542,7 @@ extern "C" int dsx_ids_fd(dsx_ctx_t* c, int fd, uint64_t off, uint64_t len, uint
 
 extern "C" int dsx_ids_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, uint64_t start,
                             const uint64_t* ends, uint64_t n, int algo, uint8_t* ids) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || (len && !h_blob) || (n && (!ends || !ids)) || bad_algo(algo)) return DSX_E_INVAL;
   MemSrc s{(const uint8_t*)h_blob};
   const int rc = run_ids(c, algo, len, fill_mem, &s, start, ends, n, ids);

@@ -32,6 +32,7 @@
 #include <type_traits>
 #include <utility>
 #include "dsx_common.h"
+#include "dsx_tasks.h"
 
 namespace dsx {
 
@@ -338,6 +339,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
 
   if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 8) {  // the task counters of the next slot
+    a.queue_next[1] = 0u;
+    a.queue_next[2] = 0u;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.overflow_next = 0u;  // (the next piece's slot)
   if constexpr (VARIANT == 4) {  // ablation: staging never filled -> zero bytes
     for (int e = threadIdx.x; e < W * NBUF * STG / 4; e += NT)
@@ -613,7 +618,13 @@ DSX_SCAN_INST_ALL(2, 1, 16, 4, false)
 // ring phases apart from the next (128 = 2*48 + 32), so the steady-state loop
 // runs three batches with phases 0, 32, 16.
 // ---------------------------------------------------------------------------
-template <int MODE, int VARIANT, int W, int SUB, int D>
+//
+// FUSE: the kernel also runs the stitch tasks of earlier queued calls
+// (*a.tasks, dsx_tasks.h) on wave slots with no region to hash: the waves
+// the grid has beyond the regions at once, the others once the regions run
+// out ("stitch behind the scan").
+// ---------------------------------------------------------------------------
+template <int MODE, int VARIANT, int W, int SUB, int D, bool FUSE>
 __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   constexpr int NC = kLine / 16;             // 16-B chunks per lane row
   constexpr int NI = kWave * kLine / 1024;   // DMA wave instructions per batch
@@ -632,6 +643,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
                                         : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
 
   if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 8) {  // the task counters of the next slot
+    a.queue_next[1] = 0u;
+    a.queue_next[2] = 0u;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.overflow_next = 0u;  // (the next piece's slot)
   if constexpr (VARIANT == 4) {
     for (int e = threadIdx.x; e < W * STG / 4; e += NT)
@@ -710,7 +725,16 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // wave-major first regions: when regions do not fill every wave slot, the
   // idle slots are single waves spread over many CUs (whose partner wave then
   // runs alone, faster) instead of whole CUs at the end of the grid
-  uint32_t region = a.wave_major ? wave * gridDim.x + blockIdx.x : blockIdx.x * W + wave;
+  // wave_major 2 (stitch behind): the waves of SIMD 3 (3 and W/2+3) come last,
+  // in pairs, so the slots without a region are whole SIMDs at the end of
+  // the grid and the stitch tasks run there beside no scan wave
+  uint32_t region;
+  if (a.wave_major == 2 && W == 8) {
+    region = (wave & 3u) == 3u ? 6u * gridDim.x + 2u * blockIdx.x + (wave >> 2)
+                               : (wave - (wave > 3u ? 1u : 0u)) * gridDim.x + blockIdx.x;
+  } else {
+    region = a.wave_major ? wave * gridDim.x + blockIdx.x : blockIdx.x * W + wave;
+  }
   const bool live = region < a.nregions;
   // The first line's DMA is issued before the table fill, so its HBM latency
   // overlaps the fill instead of following it.
@@ -759,7 +783,14 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   }
   if (kBal && threadIdx.x < W) s_prog[threadIdx.x] = 0u;
   __syncthreads();
-  if (!live) return;
+  // (trace: 6 words per wave slot after the scan's records)
+  uint64_t* const task_tr =
+      a.trace ? a.trace + (uint64_t)kScanTraceWords * gridDim.x * W + 6ull * (blockIdx.x * W + wave)
+              : nullptr;
+  if (!live) {
+    if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
+    return;
+  }
   // VARIANT 5 (diagnostic, same results): the trace records shader-clock
   // cycles from start to end and those spent waiting for the line DMA
   const uint64_t t_start = VARIANT == 5 ? __builtin_amdgcn_s_memtime()
@@ -1104,18 +1135,23 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     tr[2] = VARIANT == 5 ? (vm_wait | (copy_wait << 21) | (dma_issue << 42))
                          : (nreg_done | ((uint64_t)xcc_id << 32) | ((uint64_t)((hw_id >> 8) & 0xFF) << 40));
   }
+  // the staging line is free (the last DMA landed at vmcnt(0) above)
+  if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
 }
 
-#define DSX_SCANL_INST(W, SUB, D)                                       \
-  template __global__ void scanl_kernel<0, 0, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<1, 0, W, SUB, D>(ScanArgs);     \
-  template __global__ void scanl_kernel<2, 0, W, SUB, D>(ScanArgs);
+#define DSX_SCANL_INST(W, SUB, D)                                                   \
+  template __global__ void scanl_kernel<0, 0, W, SUB, D, false>(ScanArgs); \
+  template __global__ void scanl_kernel<1, 0, W, SUB, D, false>(ScanArgs); \
+  template __global__ void scanl_kernel<2, 0, W, SUB, D, false>(ScanArgs); \
+  template __global__ void scanl_kernel<0, 0, W, SUB, D, true>(ScanArgs);  \
+  template __global__ void scanl_kernel<1, 0, W, SUB, D, true>(ScanArgs);  \
+  template __global__ void scanl_kernel<2, 0, W, SUB, D, true>(ScanArgs);
 #if DSX_DIAG
-template __global__ void scanl_kernel<2, 1, 8, 8, 1>(ScanArgs);
-template __global__ void scanl_kernel<2, 3, 8, 8, 1>(ScanArgs);
-template __global__ void scanl_kernel<2, 4, 8, 8, 1>(ScanArgs);
-template __global__ void scanl_kernel<2, 5, 8, 8, 1>(ScanArgs);
-template __global__ void scanl_kernel<2, 6, 8, 8, 1>(ScanArgs);
+template __global__ void scanl_kernel<2, 1, 8, 8, 1, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 3, 8, 8, 1, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 4, 8, 8, 1, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 5, 8, 8, 1, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 6, 8, 8, 1, false>(ScanArgs);
 #endif
 DSX_SCANL_INST(8, 8, 1)  // D = 2 needs 16 more VGPRs than the 256 of two waves per SIMD
 

@@ -65,6 +65,51 @@ struct HostState {
 };
 constexpr uint32_t kErrCapacity = 1u;  // output capacity exceeded
 constexpr uint32_t kErrDense = 2u;     // a lane overflowed its candidate slots
+constexpr uint32_t kErrRedo = 4u;      // stitch tasks met a suspect segment: redo the call
+
+// ---- stitch behind the scan --------------------------------
+// A queued call (DSX_NO_SYNC, one piece, chain from 0) is stitched by wave
+// tasks that run inside the next calls' scans, on wave slots the scan leaves
+// idle: call j's scan kernel also walks call j-1's segments and finishes call
+// j-2 (offsets, cut list, published state).  Both read only what earlier
+// kernels wrote, so no task waits for another.
+// A task-walked segment (in the SegInfo buffer, same size): staged(k) is
+// P2 = stage[0..n2) (the chain entering from X_{k-1}, up to where it meets
+// the speculative chain S1) followed by S1's cuts spec[f1..]; cnt in all.
+struct TaskSeg {
+  uint64_t X, Z;
+  uint32_t cnt, flags;
+  uint32_t n2, f1;
+};
+struct WalkJob {
+  PieceCands pc;
+  uint64_t min, max, L;  // chain from 0 to the blob end L (one final piece)
+  uint64_t seg;          // segment k = [k*seg, min((k+1)*seg, L)) (anchor 0)
+  uint32_t nseg, scap;
+  SegInfo* seg_info;     // [nseg] (as TaskSeg)
+  uint64_t* stage;       // [nseg * scap] P2 lists
+  uint64_t* spec;        // [nseg * scap] S1 lists
+};
+struct FinishJob {
+  const SegInfo* seg_info;
+  const uint64_t* stage;
+  const uint64_t* spec;
+  const uint32_t* overflow;  // the scan's list overflow word
+  uint32_t nseg, scap;
+  uint64_t* out;             // contiguous cut list (device)
+  uint64_t out_cap;
+  HostState* host_state;     // pinned: published by the last finish task
+  uint64_t seq;
+};
+struct TaskArgs {
+  WalkJob w;
+  FinishJob f;
+  uint32_t nw, nf;       // walk / finish task counts (0: none)
+  uint32_t wseg, fseg;   // segments per walk / finish task
+  uint32_t* counter;     // task tickets (the fused scan: zeroed by the previous scan)
+  uint32_t* farrive;     // finish tasks' arrival counter (0 before, reset by the last)
+};
+constexpr uint32_t kTaskCand = 2048;  // candidates a walk task stages (8 KiB of LDS)
 constexpr uint64_t kSeamPeerFailed = 0x7FFFFFFFFFFFFFFFull;  // seam_resolve_kernel statuses
 constexpr uint64_t kSeamRedo = 0x7FFFFFFFFFFFFFFEull;
 
@@ -95,6 +140,9 @@ struct StitchArgs {
   uint64_t init_carry;    // init: the chain origin
   uint32_t init;          // first piece of a call: walk_kernel resets the chain state
   uint32_t pad_init;
+  // finish_kernel's arrival counter (0 between launches): the last workgroup
+  // to arrive publishes, so a published seq means the cut list is complete
+  uint32_t* arrive;
 };
 
 }  // namespace dsx

@@ -25,12 +25,12 @@
 //   K4 gather contiguous cut list.
 #include <hip/hip_runtime.h>
 
+#include "dsx_chain.h"
 #include "dsx_common.h"
 #include "dsx_stitch.h"
+#include "dsx_tasks.h"
 
 namespace dsx {
-
-constexpr uint64_t kNone = ~0ull;
 
 // ---- candidate sources -----------------------------------------------------
 // Sorted candidates in LDS, positions lo + c[i].  first_in(a, b) returns the
@@ -61,120 +61,6 @@ struct LdsSrc {
     j = l;
   }
 };
-
-// The same source searched by a whole wavefront: 64 candidates per LDS read
-// and a ballot, so a chain step costs one LDS round trip instead of one per
-// candidate passed (the walks are latency-bound: one chain per wave).
-struct WaveLdsSrc {
-  const uint32_t* c;
-  uint32_t n;
-  uint32_t base;  // window start: lane l holds c[base + l] in v
-  uint64_t lo;
-  uint32_t lane;
-  uint32_t v;
-  __device__ void load() { v = base + lane < n ? c[base + lane] : 0xFFFFFFFFu; }
-  // first candidate > a (relative ar), searching forward from the window;
-  // returns its relative offset or 0xFFFFFFFF.  Steps of a chain advance by
-  // about one candidate, so most calls hit the window already in registers.
-  __device__ uint32_t next_after(uint64_t ar) {
-    const uint32_t ar32 = ar > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)ar;
-    while (true) {
-      const uint64_t m = __ballot(v > ar32);
-      if (m) {
-        const uint32_t f = (uint32_t)__builtin_ctzll(m);
-        if (base + f >= n) return 0xFFFFFFFFu;
-        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)f);
-      }
-      if (base + 64u >= n) return 0xFFFFFFFFu;
-      base += 64u;
-      load();
-    }
-  }
-  __device__ uint32_t next_after32(uint32_t ar32) {
-    while (true) {
-      const uint64_t m = __ballot(v > ar32);
-      if (m) {
-        const uint32_t f = (uint32_t)__builtin_ctzll(m);
-        if (base + f >= n) return 0xFFFFFFFFu;
-        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)f);
-      }
-      if (base + 64u >= n) return 0xFFFFFFFFu;
-      base += 64u;
-      load();
-    }
-  }
-  __device__ uint64_t first_in(uint64_t a, uint64_t b) {
-    const uint32_t r = next_after(a - lo);  // a >= lo always (a = s+min, s >= lo)
-    if (r != 0xFFFFFFFFu) {
-      const uint64_t p = lo + r;
-      if (p <= b) return p;
-    }
-    return kNone;
-  }
-  // position the window at the first candidate > a
-  __device__ void seek(uint64_t a) {
-    base = 0;
-    load();
-    const uint64_t ar = a < lo ? 0 : a - lo;
-    const uint32_t ar32 = ar > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)ar;
-    while (base + 64u < n && __ballot(v > ar32) == 0) {
-      base += 64u;
-      load();
-    }
-  }
-};
-
-// wave-uniform 64-bit value (scalar registers, scalar control flow)
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// The chain rule in 32-bit coordinates relative to a walk workgroup's `lo`
-// (its candidates and segments span far less than 4 GiB): every chain step is
-// a handful of scalar 32-bit operations instead of 64-bit vector compares.
-constexpr uint32_t kRelUndet = 0xFFFFFFFFu;
-constexpr uint32_t kRelClamp = 0xFFFFFFF0u;
-struct RelChain {
-  uint32_t min, max, L, PE;  // L, PE relative to lo, clamped to kRelClamp
-  bool is_last;
-  // the same bounds folded for branch-free steps: a chain at s >= tail_at
-  // ends at L (chunker.go:215-217: len - s <= min); steps are capped at
-  // lim_cap (L: chunker.go:221); a bound beyond undet_at is undetermined
-  // (non-final piece).  Unused bounds are 0xFFFFFFFF.
-  uint32_t tail_at, lim_cap, undet_at, end_at;
-};
-__device__ __forceinline__ uint32_t rel_clamp(uint64_t v, uint64_t lo) {
-  return v <= lo ? 0u : (v - lo >= kRelClamp ? kRelClamp : (uint32_t)(v - lo));
-}
-__device__ __forceinline__ RelChain rel_chain(const ChainParams& w, uint64_t lo) {
-  // min/max clamped to 2^30: a walk workgroup spans far less, so a bound
-  // beyond 2^30 decides exactly like the real one (the chain leaves the
-  // segment either way), and s + max never overflows 32 bits
-  RelChain r;
-  r.min = w.min < (1ull << 30) ? (uint32_t)w.min : (1u << 30);
-  r.max = w.max < (1ull << 30) ? (uint32_t)w.max : (1u << 30);
-  r.L = rel_clamp(w.L, lo);
-  r.PE = rel_clamp(w.PE, lo);
-  r.is_last = w.is_last != 0;
-  r.tail_at = r.is_last ? (r.L > r.min ? r.L - r.min : 0u) : 0xFFFFFFFFu;
-  r.lim_cap = r.is_last ? r.L : 0xFFFFFFFFu;
-  r.undet_at = r.is_last ? 0xFFFFFFFFu : r.PE;
-  r.end_at = r.is_last ? r.L : 0xFFFFFFFFu;
-  return r;
-}
-// next(s) of chunker.go:206-277 for a relative chain position s (< L when
-// is_last); kRelUndet if the successor depends on bytes beyond the piece.
-// Straight-line scalar code around one ballot step (the walks are
-// latency-bound: every branch and wait is on the chain's critical path).
-__device__ __forceinline__ uint32_t rel_next(uint32_t s, WaveLdsSrc& src, const RelChain& w) {
-  if (s >= w.tail_at) return w.L;                  // chunker.go:215-217
-  const uint32_t lim = min(s + w.max, w.lim_cap);  // chunker.go:221
-  const uint32_t c = src.next_after32(s + w.min);  // chunker.go:259-271
-  if (c <= lim) return c;                          // (none = 0xFFFFFFFF > lim)
-  return lim > w.undet_at ? kRelUndet : lim;       // chunker.go:276
-}
 
 // Candidates straight from the scan's per-region sorted lists (global
 // memory); used by the sequential repair only.
@@ -219,14 +105,6 @@ __device__ __forceinline__ uint64_t next_cut(uint64_t s, Src& src, const ChainPa
   if (c != kNone) return c;
   if (!w.is_last && lim > w.PE) return kUndet;
   return lim;  // chunker.go:276
-}
-
-__device__ __forceinline__ uint64_t seg_start(const StitchArgs& a, uint64_t s0, uint32_t k) {
-  return k == 0 ? s0 : a.anchor + (uint64_t)k * a.seg;
-}
-__device__ __forceinline__ uint64_t seg_end(const StitchArgs& a, uint32_t k) {
-  if (k + 1 >= a.nseg) return a.chain.is_last ? a.chain.L : a.chain.PE;
-  return a.anchor + (uint64_t)(k + 1) * a.seg;
 }
 
 // ---- K2: per-segment speculative walks ------------------------------------
@@ -490,9 +368,31 @@ __device__ void publish(const StitchArgs& a, const DevState* st) {
   h->repaired = st->repaired;
   h->done = st->done;
   h->err = st->err;
+  // seq last, after a system-scope release: a host that polls seq (queued
+  // calls, dsx_result) without synchronising the stream then reads the
+  // fields of this piece, and finish_kernel's publisher arrives last, so the
+  // cut list is complete too
+  __threadfence_system();
   h->seq = a.seq;
-  // (no system fence: the host reads this after the stream synchronises, and
-  // the end-of-kernel release makes the writes visible)
+}
+
+// finish_kernel: every workgroup calls this once, after its last global
+// write; true in the last workgroup to arrive (which then sees every other
+// workgroup's writes) and the counter is back at 0 for the next launch.
+__device__ bool arrive_last(const StitchArgs& a) {
+  __shared__ uint32_t s_is_last;
+  __threadfence();  // release this workgroup's writes (device scope)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t n = atomicAdd(a.arrive, 1u);
+    s_is_last = n + 1u == gridDim.x ? 1u : 0u;
+    if (s_is_last) {
+      atomicExch(a.arrive, 0u);
+      __threadfence();  // acquire the other workgroups' writes
+    }
+  }
+  __syncthreads();
+  return s_is_last != 0;
 }
 
 __device__ uint32_t bsearch_u64(const uint64_t* v, uint32_t n, uint64_t x) {
@@ -507,7 +407,7 @@ __device__ uint32_t bsearch_u64(const uint64_t* v, uint32_t n, uint64_t x) {
 // K3's body for a workgroup of NT threads (fixup_kernel, and the repair path
 // of fixup_fast_kernel).
 template <int NT>
-__device__ void fixup_body(const StitchArgs& a) {
+__device__ void fixup_body(const StitchArgs& a, bool do_publish = true) {
   __shared__ uint32_t s_flag_cnt;
   __shared__ uint64_t s_part[NT / 64];
   __shared__ int s_last_seg;
@@ -519,7 +419,7 @@ __device__ void fixup_body(const StitchArgs& a) {
       st->active = 0;
       st->piece_cuts = 0;
       if (*a.pc.overflow) st->err |= kErrDense;
-      publish(a, st);
+      if (do_publish) publish(a, st);
     }
     return;
   }
@@ -667,7 +567,7 @@ __device__ void fixup_body(const StitchArgs& a) {
     if (tot > a.out_cap) st->err |= kErrCapacity;
     st->total = tot;
     st->active = 1;
-    publish(a, st);
+    if (do_publish) publish(a, st);
   }
 }
 
@@ -871,9 +771,8 @@ __global__ __launch_bounds__(kFinThreads) void finish_kernel(StitchArgs a) {
       v[q] = a.stage[(uint64_t)k * a.scap + (lane < sc1 ? lane : sc1)];
     }
   }
-  const bool last_wg = blockIdx.x == gridDim.x - 1;
   if (skip) {  // what fixup_kernel publishes when the piece was not walked
-    if (last_wg && tid == 0) {
+    if (arrive_last(a) && tid == 0) {
       st->active = 0;
       st->piece_cuts = 0;
       if (*a.pc.overflow) st->err |= kErrDense;
@@ -900,20 +799,24 @@ __global__ __launch_bounds__(kFinThreads) void finish_kernel(StitchArgs a) {
     }
   }
   if (__syncthreads_or(bad)) {  // a suspect segment: workgroup 0 does it all
-    if (blockIdx.x != 0) return;
-    fixup_body<NT>(a);
-    __threadfence_block();
-    __syncthreads();
-    if (!st->active || (st->err & kErrCapacity)) return;
-    for (uint32_t k = tid; k < T; k += NT) {
-      const uint32_t scnt = (a.seg_info[k].flags & kBad) ? 0u : a.seg_info[k].cnt;
-      const uint32_t rc = a.rep_cnt[k], rf = a.rep_from[k];
-      const uint64_t off = a.out_off[k];
-      const uint64_t* rep = a.rep + (uint64_t)k * a.scap;
-      const uint64_t* stg = a.stage + (uint64_t)k * a.scap;
-      for (uint32_t i = 0; i < rc; ++i) a.out[off + i] = rep[i];
-      for (uint32_t i = rf; i < scnt; ++i) a.out[off + rc + (i - rf)] = stg[i];
+    if (blockIdx.x == 0) {
+      fixup_body<NT>(a, false);
+      __threadfence_block();
+      __syncthreads();
+      if (st->active && !(st->err & kErrCapacity)) {
+        for (uint32_t k = tid; k < T; k += NT) {
+          const uint32_t scnt = (a.seg_info[k].flags & kBad) ? 0u : a.seg_info[k].cnt;
+          const uint32_t rc = a.rep_cnt[k], rf = a.rep_from[k];
+          const uint64_t off = a.out_off[k];
+          const uint64_t* rep = a.rep + (uint64_t)k * a.scap;
+          const uint64_t* stg = a.stage + (uint64_t)k * a.scap;
+          for (uint32_t i = 0; i < rc; ++i) a.out[off + i] = rep[i];
+          for (uint32_t i = rf; i < scnt; ++i) a.out[off + rc + (i - rf)] = stg[i];
+        }
+      }
     }
+    // the state workgroup 0 wrote, published by whichever workgroup arrives last
+    if (arrive_last(a) && tid == 0) publish(a, st);
     return;
   }
   // every staged list is the true chain: counts -> offsets
@@ -975,7 +878,9 @@ __global__ __launch_bounds__(kFinThreads) void finish_kernel(StitchArgs a) {
         a.out[s_off[k] + i] = a.stage[(uint64_t)k * a.scap + i];
     }
   }
-  if (last_wg && tid == 0) {
+  // every workgroup computed the same state; the last to arrive writes and
+  // publishes it
+  if (arrive_last(a) && tid == 0) {
     if (s_last_seg >= 0) st->carry = s_carry;
     if (a.chain.is_last && st->carry >= a.chain.L) st->done = 1;
     st->piece_cuts = piece;
@@ -989,6 +894,17 @@ template __global__ void finish_kernel<1>(StitchArgs);
 template __global__ void finish_kernel<2>(StitchArgs);
 template __global__ void finish_kernel<4>(StitchArgs);
 template __global__ void finish_kernel<8>(StitchArgs);
+
+// The stitch tasks of queued calls that no later scan carried (flush_behind):
+// one task per wave, finish tasks first.
+__global__ __launch_bounds__(256) void stitch_task_kernel(TaskArgs b) {
+  __shared__ __attribute__((aligned(16))) uint32_t cand[4 * kTaskCand];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * 4u + wave;
+  if (t < b.nf) finish_task(b.f, t, b.fseg, b.nf, b.farrive, lane);
+  else if (t - b.nf < b.nw) walk_task(b.w, t - b.nf, b.wseg, cand + wave * kTaskCand, lane);
+}
 
 // The chain state of a stitch-only pass (a shard re-walked from its true
 // entry over kept candidate lists; normally the scan initialises it).

@@ -310,6 +310,7 @@ void stream_release(dsx_ctx* c) {
 }
 
 extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
+  DSX_FLUSH_BEHIND(c);
   if (!c || !p) return DSX_E_INVAL;
   auto& s = c->st;
   // one stream per context (its scratch and carried state live here): a

@@ -1,0 +1,215 @@
+"""Stitch behind the scan: queued (DSX_NO_SYNC) dsx_cut_device calls whose
+walk and finish run as tasks inside the next calls' scans.
+
+Every call's cut list must equal the oracle's chain (chunker.go:206-277)
+whatever runs between the calls: more fused calls, calls that cannot be
+fused (a pointer off the 128-B grid, a dense-candidate parameter set), a
+dsx_sync, a synchronous call, collection at every queue depth.  Suspect
+segments (seams inside zero runs with short segments) take the redo path.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as o
+
+pytestmark = pytest.mark.gpu
+
+MIN, AVG, MAX = 16 * 1024, 64 * 1024, 256 * 1024
+
+
+def _dev(arr, pad=0):
+    import torch
+    t = torch.empty(arr.size + pad, dtype=torch.uint8, device="cuda")
+    t[pad:].copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.uint8)))
+    torch.cuda.synchronize()
+    return t, t.data_ptr() + pad
+
+
+class Queue:
+    """Queued calls on one context, collected oldest first."""
+
+    def __init__(self, ctx):
+        from desync_amd import _lib
+        self.ctx, self.L, self.lib = ctx, _lib.lib(), _lib
+        self.pending = []  # (ref, out tensor, keepalive)
+
+    def submit(self, arr, mn=MIN, av=AVG, mx=MAX, pad=0, flags=0):
+        import torch
+        import desync_amd
+        t, ptr = _dev(arr, pad)
+        p = desync_amd.Params(mn, av, mx)
+        out = torch.empty(arr.size // mn + 4, dtype=torch.int64, device="cuda")
+        cnt = ctypes.c_uint64()
+        self.lib.check(self.L.dsx_cut_device(
+            self.ctx.h, ctypes.c_void_p(ptr), arr.size, ctypes.byref(p.c),
+            ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(cnt),
+            self.lib.DSX_OUT_DEVICE | self.lib.DSX_NO_SYNC | flags), self.ctx.h)
+        self.pending.append((o.chunk_stream(arr, mn, av, mx), out, (t, p)))
+
+    def collect(self):
+        ref, out, _ = self.pending.pop(0)
+        cnt = ctypes.c_uint64()
+        self.lib.check(self.L.dsx_result(self.ctx.h, ctypes.byref(cnt)), self.ctx.h)
+        assert cnt.value == ref.size
+        got = out[:cnt.value].cpu().numpy().astype(np.uint64)
+        assert np.array_equal(got, ref)
+
+
+@pytest.fixture
+def fctx(monkeypatch):
+    """A context with the stitch behind the scan switched on (DSX_FUSE=1)."""
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_FUSE", "1")
+    ctx = _lib.Context(0)
+    yield ctx
+    ctx.close()
+
+
+def _blobs():
+    rng = np.random.default_rng(5)
+    dense_blk = None
+    P = o.params(MIN, AVG, MAX)
+    while dense_blk is None:  # a 48-byte period whose window hash is a candidate
+        blk = rng.integers(0, 256, 48, dtype=np.uint8)
+        if o.window_hash(bytes(blk)) % P.d == P.d - 1:
+            dense_blk = blk
+    return {
+        "u1": o.synth_uniform(61, 0, (1 << 20) + 12345),
+        "u40": o.synth_uniform(62, 0, (40 << 20) + 7),
+        "u300": o.synth_uniform(63, 0, (300 << 20) + 4097),
+        "zeros": np.zeros((24 << 20) + 5, np.uint8),
+        "mixed": np.concatenate([o.synth_uniform(64, 0, 3 << 20), np.zeros(5 << 20, np.uint8),
+                                 o.synth_uniform(65, 0, (7 << 20) + 3)]),
+        "periodic": np.tile(dense_blk, (3 << 20) // 48),
+        "tiny": o.synth_uniform(66, 0, 1000),
+    }
+
+
+def test_behind_sequence(fctx):
+    """A run of queued calls, fused and not, collected at depths 1..8."""
+    from desync_amd import _lib
+    b = _blobs()
+    q = Queue(fctx)
+    plan = ["u40", "u1", "u300", "zeros", "mixed", "u40", "tiny", "u1", "periodic",
+            "u300", "mixed", "zeros"]
+    for depth in (1, 2, 3, 4, 8):
+        for name in plan:
+            while len(q.pending) >= depth:
+                q.collect()
+            q.submit(b[name])
+        while q.pending:
+            q.collect()
+    # other parameters and a pointer off the line grid (not fused: flushes)
+    for depth in (3, 5):
+        q.submit(b["u40"])
+        q.submit(b["u40"], 4096, 8192, 65536)
+        q.submit(b["u1"], pad=1)
+        q.submit(b["mixed"], 64 << 10, 1 << 20, 4 << 20)
+        q.submit(b["u300"])
+        if depth == 5:
+            _lib.check(_lib.lib().dsx_sync(fctx.h), fctx.h)  # flushes the calls behind
+        q.submit(b["u40"], 1000, 8000, 64000)  # dense candidates: not fused
+        q.submit(b["u1"])
+        while q.pending:
+            q.collect()
+
+
+def test_behind_interleaved_sync_calls(fctx):
+    """A synchronous call and a chunk-ID call between queued ones run after
+    the stitches still behind, and every result stays exact."""
+    import desync_amd
+    b = _blobs()
+    q = Queue(fctx)
+    q.submit(b["u40"])
+    q.submit(b["mixed"])
+    t, ptr = _dev(b["u300"])
+    got = desync_amd.cut_device(ptr, b["u300"].size, MIN, AVG, MAX, ctx=fctx)
+    assert np.array_equal(got, o.chunk_stream(b["u300"], MIN, AVG, MAX))
+    q.submit(b["zeros"])
+    ids = desync_amd.chunk_ids(ptr, b["u300"].size, got[:50], 0, ctx=fctx)
+    assert len(ids) == 50
+    q.submit(b["u1"])
+    while q.pending:
+        q.collect()
+
+
+def test_behind_redo_on_suspect_segments(monkeypatch):
+    """Short segments (64 KiB floor, 4 x max) with the true chain inside zero
+    runs off the segment grid: seams that do not converge.  The tasks publish
+    kErrRedo and dsx_result redoes the call with fixup_kernel's repair."""
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_SEG_FLOOR", "65536")
+    monkeypatch.setenv("DSX_FUSE", "1")
+    ctx = _lib.Context(0)
+    try:
+        rng = np.random.default_rng(11)
+        null = np.zeros(4 * MAX, np.uint8)
+        r1 = rng.integers(0, 256, 4 * MAX, dtype=np.uint8)
+        d = np.concatenate([r1[:12345], null, null, null, r1, null, r1])
+        u = o.synth_uniform(67, 0, 9 << 20)
+        q = Queue(ctx)
+        for _ in range(3):
+            q.submit(d)
+            q.submit(u)
+        while q.pending:
+            q.collect()  # d: redone on the general path, which repairs
+            assert ctx.stats().repaired_segments > 0
+            q.collect()
+    finally:
+        ctx.close()
+
+
+def test_behind_timed_calls(fctx):
+    """DSX_TIMED fused calls report the scan kernel's time (it carries the
+    stitch tasks of the calls behind it) and no separate stitch time."""
+    from desync_amd import _lib
+    b = _blobs()
+    q = Queue(fctx)
+    for name in ("u40", "u40", "u40", "u40"):
+        q.submit(b[name], flags=_lib.DSX_TIMED)
+    while q.pending:
+        q.collect()
+        st = fctx.stats()
+        assert 0 < st.scan_ms < 100 and st.stitch_ms == 0
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_bench_steady_state_counts(monkeypatch, fuse):
+    """bench.py's shape: 1 GiB uniform jobs queued 4 deep on one context give
+    the same cut list as the oracle, with and without the fused stitch."""
+    import torch
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_FUSE", fuse)
+    ctx = _lib.Context(0)
+    try:
+        n = 1 << 30
+        arr = o.synth_uniform(1, 0, n)
+        ref = o.chunk_parallel(arr, MIN, AVG, MAX, 16)
+        t = torch.from_numpy(arr).to("cuda")
+        del arr
+        import desync_amd
+        p = desync_amd.Params(MIN, AVG, MAX)
+        L = _lib.lib()
+        outs = [torch.empty(n // MIN + 4, dtype=torch.int64, device="cuda") for _ in range(4)]
+        cnt = ctypes.c_uint64()
+        pend = []
+        for s in range(12):
+            if len(pend) == 4:
+                i = pend.pop(0)
+                _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
+                assert cnt.value == ref.size
+                assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
+            _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(t.data_ptr()), n, ctypes.byref(p.c),
+                                        ctypes.c_void_p(outs[s % 4].data_ptr()), n // MIN + 4,
+                                        ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
+                       ctx.h)
+            pend.append(s % 4)
+        while pend:
+            i = pend.pop(0)
+            _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
+            assert cnt.value == ref.size
+            assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
+    finally:
+        ctx.close()
