@@ -248,12 +248,15 @@ __device__ __forceinline__ void hash_span(const uint32_t* w, uint32_t& h, uint32
       const int k = j * SUB + i;
       const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8);
       const uint32_t addr = __builtin_amdgcn_perm(w[k >> 2], slot8, sel);
-      L[j & 1][i] = *reinterpret_cast<const uint64_t*>(tbl + addr);
+      if constexpr (VARIANT == 7)
+        L[j & 1][i] = *reinterpret_cast<const uint32_t*>(tbl + addr);
+      else
+        L[j & 1][i] = *reinterpret_cast<const uint64_t*>(tbl + addr);
     }
   };
   auto compute = [&](int j) {
     lookups_landed<SUB>(L[j & 1]);
-    constexpr bool kTest = TEST && (VARIANT == 0 || VARIANT == 4);
+    constexpr bool kTest = TEST && (VARIANT == 0 || VARIANT == 4 || VARIANT == 7);
     uint64_t m[SUB];   // MODE 0/1: per-byte ballots
     uint32_t t[SUB];   // MODE 2: prefilter values
 #pragma unroll
@@ -262,9 +265,12 @@ __device__ __forceinline__ void hash_span(const uint32_t* w, uint32_t& h, uint32
       // rotl1(h) ^ T[in] ^ Trot[out]: one v_alignbit + one three-input
       // v_bitop3_b32 (xor3, gfx950)
       const int rk = (PH + k) % 48;
+      // (VARIANT 7: 4-byte table entries, the ring holds T and the outgoing
+      // term is rotated here)
+      const uint32_t outv = VARIANT == 7 ? __builtin_amdgcn_alignbit(ring[rk], ring[rk], 16) : ring[rk];
       h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31),
-                                      (uint32_t)L[j & 1][i], ring[rk], 0x96);
-      ring[rk] = (uint32_t)(L[j & 1][i] >> 32);
+                                      (uint32_t)L[j & 1][i], outv, 0x96);
+      ring[rk] = VARIANT == 7 ? (uint32_t)L[j & 1][i] : (uint32_t)(L[j & 1][i] >> 32);
       if constexpr (kTest && MODE == 2) t[i] = mode2_t_mad(h, tc.inv, (uint64_t)tc.tadd);
       else if constexpr (kTest) m[i] = __ballot(is_cand<MODE>(h, tc));
     }
@@ -655,7 +661,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t slot8 = (lane & 31u) * 8u;
+  // (VARIANT 7: 64 slots of 4 B per byte value instead of 32 of 8 B)
+  const uint32_t slot8 = VARIANT == 7 ? lane * 4u : (lane & 31u) * 8u;
   uint8_t* stage = lds + kTableBytes + wave * STG;
   // Waves w and w + W/2 share a SIMD (waves are placed on the SIMDs
   // cyclically).  VALU issue favours the older wave, so left alone the
@@ -775,10 +782,18 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     uint2 t;
     t.x = tv;
     t.y = __builtin_amdgcn_alignbit(tv, tv, 16);
+    if constexpr (VARIANT == 7) {
 #pragma unroll
-    for (int k = 0; k < (32 + TPV - 1) / TPV; ++k) {
-      const uint32_t slot = (threadIdx.x >> 8) + (uint32_t)(k * TPV);
-      if (slot < 32u) *reinterpret_cast<uint2*>(lds + v * 256u + slot * 8u) = t;
+      for (int k = 0; k < (64 + TPV - 1) / TPV; ++k) {
+        const uint32_t slot = (threadIdx.x >> 8) + (uint32_t)(k * TPV);
+        if (slot < 64u) *reinterpret_cast<uint32_t*>(lds + v * 256u + slot * 4u) = tv;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < (32 + TPV - 1) / TPV; ++k) {
+        const uint32_t slot = (threadIdx.x >> 8) + (uint32_t)(k * TPV);
+        if (slot < 32u) *reinterpret_cast<uint2*>(lds + v * 256u + slot * 8u) = t;
+      }
     }
   }
   if (kBal && threadIdx.x < W) s_prog[threadIdx.x] = 0u;
@@ -927,7 +942,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int k = (g % 16) * 8 + q;  // byte within the line
-        L[g % NL][q] = *reinterpret_cast<const uint64_t*>(lds + lookup_addr(w[k >> 2], slot8, k & 3));
+        if constexpr (VARIANT == 7)
+          L[g % NL][q] = *reinterpret_cast<const uint32_t*>(lds + lookup_addr(w[k >> 2], slot8, k & 3));
+        else
+          L[g % NL][q] = *reinterpret_cast<const uint64_t*>(lds + lookup_addr(w[k >> 2], slot8, k & 3));
       }
     };
     auto compute_sub = [&](auto gc, uint32_t o0) __attribute__((always_inline)) {
@@ -938,14 +956,16 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         return;
       }
       lookups_landed<8>(L[g % NL]);
-      constexpr bool kTest = VARIANT == 0 || VARIANT == 4 || VARIANT == 5;
+      constexpr bool kTest = VARIANT == 0 || VARIANT == 4 || VARIANT == 5 || VARIANT == 7;
       uint32_t t[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int rk = (g * 8 + q) % 48;
+        const uint32_t outv =
+            VARIANT == 7 ? __builtin_amdgcn_alignbit(ring[rk], ring[rk], 16) : ring[rk];
         h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31),
-                                        (uint32_t)L[g % NL][q], ring[rk], 0x96);
-        ring[rk] = (uint32_t)(L[g % NL][q] >> 32);
+                                        (uint32_t)L[g % NL][q], outv, 0x96);
+        ring[rk] = VARIANT == 7 ? (uint32_t)L[g % NL][q] : (uint32_t)(L[g % NL][q] >> 32);
         if constexpr (kTest) {
           if constexpr (MODE == 2) t[q] = h * tcv.ninv;  // t + 1: one v_mul_lo_u32
           else t[q] = is_cand<MODE>(h, tcv) ? 0u : 0xFFFFFFFFu;
@@ -1152,6 +1172,7 @@ template __global__ void scanl_kernel<2, 3, 8, 8, 1, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 4, 8, 8, 1, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 5, 8, 8, 1, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 6, 8, 8, 1, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 7, 8, 8, 1, false>(ScanArgs);
 #endif
 DSX_SCANL_INST(8, 8, 1)  // D = 2 needs 16 more VGPRs than the 256 of two waves per SIMD
 
