@@ -732,6 +732,17 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   return DSX_OK;
 }
 
+// The piece's state into the pinned host slot after its stitch (the host
+// polls it for queued calls, reads it after a sync otherwise).
+static int launch_publish(dsx_ctx* c, const StitchArgs& ta) {
+  if (ta.host_state) {
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, c->stream, ta);
+    HIPCHK(c, hipGetLastError());
+  }
+  c->last_finish = ta.host_state != nullptr;
+  return DSX_OK;
+}
+
 // walk -> fixup -> gather for one piece whose candidates are in pc.
 int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t P, uint64_t len,
                   bool is_last, uint64_t seq, bool trace) {
@@ -789,7 +800,6 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   ta.seq = seq;
   ta.init = c->init_pending ? 1u : 0u;  // the call's first piece: walk_kernel resets the state
   ta.init_carry = c->init_carry;
-  ta.arrive = c->overflow.p + kArriveWord;
   c->init_pending = false;
   c->last_finish = false;
   const uint32_t walk_grid = (uint32_t)((nseg + spg - 1) / spg);
@@ -810,8 +820,7 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
     else if (nseg <= 1024) hipLaunchKernelGGL(finish_kernel<4>, fg, dim3(256), 0, c->stream, ta);
     else hipLaunchKernelGGL(finish_kernel<8>, fg, dim3(256), 0, c->stream, ta);
     HIPCHK(c, hipGetLastError());
-    c->last_finish = true;  // its publisher arrives last: the host may poll the seq
-    return DSX_OK;
+    return launch_publish(c, ta);
   }
   if (c->fixup_fast && nseg <= 8 * 1024) {
     if (nseg <= 1024) hipLaunchKernelGGL(fixup_fast_kernel<1>, dim3(1), dim3(1024), 0, c->stream, ta);
@@ -824,7 +833,7 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(gather_kernel, dim3((uint32_t)nseg), dim3(256), 0, c->stream, ta);
   HIPCHK(c, hipGetLastError());
-  return DSX_OK;
+  return launch_publish(c, ta);
 }
 
 // Runs a whole device-resident blob [origin.., origin+len) through the engine.

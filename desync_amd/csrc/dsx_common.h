@@ -86,7 +86,7 @@ constexpr int kLine = 128;
 constexpr int kScanTraceWords = 6;  // per wave: start, end, info, entry, region-end cycles, region-start waits
 constexpr int kQueueSlots = 4;                  // overflow / queue slots (piece seq mod 4)
 constexpr int kQueueWords = 32 + kQueueSlots * 256;  // overflow words + 4 x 8 queue counters
-constexpr int kArriveWord = 16;                 // finish_kernel's arrival counter (word 16)
+constexpr int kArriveWord = 16;                 // stitch_task_kernel's arrival counter (word 17)
 constexpr uint32_t kLineLaneMax = 384u * 170u;  // 65280
 
 // Sentinel for "successor depends on bytes beyond the piece" (non-final piece).

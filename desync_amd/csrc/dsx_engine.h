@@ -33,6 +33,7 @@ __global__ void fixup_fast_kernel(StitchArgs a);
 template <int PER>
 __global__ void finish_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);
+__global__ void publish_kernel(StitchArgs a);
 __global__ void state_init_kernel(DevState* st, uint64_t carry);
 __global__ void gen_uniform_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed);
 __global__ void gen_dedup_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed,
@@ -156,7 +157,7 @@ struct dsx_ctx {
   uint64_t last_region_bytes = 0;  // geometry of the last enqueued piece's region lists
   uint32_t last_nregions = 0, last_region_cap = 0;
   uint64_t init_carry = 0;
-  bool last_finish = false;  // the last stitch ended with finish_kernel (publishes last)
+  bool last_finish = false;  // the last stitch ended with publish_kernel (the host may poll)
   // stitch behind the scan (DSX_FUSE, default on): queued one-piece calls
   // whose walk (walked = false) or finish (walked = true) runs as tasks in
   // the next queued call's scan; flush_behind() launches them on their own

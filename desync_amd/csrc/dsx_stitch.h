@@ -140,9 +140,6 @@ struct StitchArgs {
   uint64_t init_carry;    // init: the chain origin
   uint32_t init;          // first piece of a call: walk_kernel resets the chain state
   uint32_t pad_init;
-  // finish_kernel's arrival counter (0 between launches): the last workgroup
-  // to arrive publishes, so a published seq means the cut list is complete
-  uint32_t* arrive;
 };
 
 }  // namespace dsx

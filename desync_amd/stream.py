@@ -75,6 +75,9 @@ class MemoryStore:
             self.chunks[chunk.ID()] = chunk.Data()
 
 
+_BATCH = 64  # chunks per hand-off to the store workers
+
+
 def ChunkStream(ctx, c, ws, n):
     """index.go:138-234.  ``c`` is a desync_amd Chunker that has not produced
     a chunk yet (its IDs are switched on here), ``ws`` a store, ``n`` the
@@ -89,24 +92,29 @@ def ChunkStream(ctx, c, ws, n):
     # the reference's channel to n store goroutines (index.go:150-182): a
     # bounded queue read by n threads; the first store error stops the
     # producer, the workers drain what is queued without storing it
+    # (chunks travel in groups of up to _BATCH: a queue hand-off per chunk
+    # cost more than the rest of the per-chunk work; each chunk is still
+    # stored on its own, in stream order within a group)
     work = queue.Queue(maxsize=4 * nw)
     errors = []
 
     def worker():
         while True:
-            ch = work.get()
-            if ch is None:
+            group = work.get()
+            if group is None:
                 return
-            if errors:
-                continue
-            try:
-                storage.StoreChunk(ch)
-            except BaseException as e:  # noqa: BLE001 -- re-raised by the producer
-                errors.append(e)
+            for ch in group:
+                if errors:
+                    break
+                try:
+                    storage.StoreChunk(ch)
+                except BaseException as e:  # noqa: BLE001 -- re-raised by the producer
+                    errors.append(e)
 
     threads = [threading.Thread(target=worker, daemon=True) for _ in range(nw)]
     for t in threads:
         t.start()
+    group = []
     try:
         while not errors:
             if ctx is not None and getattr(ctx, "done", lambda: False)():
@@ -119,8 +127,13 @@ def ChunkStream(ctx, c, ws, n):
                 raise RuntimeError("chunker produced a chunk without a GPU chunk ID")
             data = bytes(b)  # slices.Clone (index.go:196-200)
             chunks.append(IndexChunk(cid, start, len(data)))
-            work.put(Chunk(cid, data))
+            group.append(Chunk(cid, data))
+            if len(group) >= _BATCH:
+                work.put(group)
+                group = []
     finally:
+        if group and not errors:
+            work.put(group)
         for _ in threads:
             work.put(None)
         for t in threads:
