@@ -563,6 +563,12 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.queue_next = c->overflow.p + 32 + 256 * ((seq + 1) % kQueueSlots);
   sa.wave_major = c->wave_major ? (cc.behind ? 2u : 1u) : 0u;
   sa.nt_loads = (uint32_t)c->scan_nt;
+  if (c->pub_host) {  // the previous queued piece's state, published by this scan
+    sa.pub_state = c->state.p;
+    sa.pub_host = c->pub_host;
+    sa.pub_seq = c->pub_seq;
+    c->pub_host = nullptr;
+  }
   tb.counter = sa.queue + 1;  // (zeroed by the previous scan, with the queue)
   tb.farrive = sa.queue + 2;
 
@@ -603,6 +609,9 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   // the region lists this scan writes were read by the stitch two pieces ago
   if (split) HIPCHK(c, hipStreamWaitEvent(ss, c->ev_stitch[par], 0));
   if (c->timing) HIPCHK(c, hipEventRecord(c->pev[3 * pi], ss));
+#if DSX_DIAG
+  if (getenv("DSX_NOOP_BEFORE_SCAN")) hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, ss);
+#endif
   {
     const uint64_t need_wg = std::max<uint64_t>(1, (nregions + W - 1) / W);
     // (stitch behind: every CU, so the wave slots beyond the regions -- spread
@@ -735,11 +744,28 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
 // The piece's state into the pinned host slot after its stitch (the host
 // polls it for queued calls, reads it after a sync otherwise).
 static int launch_publish(dsx_ctx* c, const StitchArgs& ta) {
-  if (ta.host_state) {
-    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, c->stream, ta);
-    HIPCHK(c, hipGetLastError());
-  }
   c->last_finish = ta.host_state != nullptr;
+  if (!ta.host_state) return DSX_OK;
+  if (c->defer_publish) {  // a queued call: the next scan publishes it
+    c->pub_host = ta.host_state;
+    c->pub_seq = ta.seq;
+    return DSX_OK;
+  }
+  hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, c->stream, ta);
+  HIPCHK(c, hipGetLastError());
+  return DSX_OK;
+}
+
+int flush_publish(dsx_ctx* c) {
+  if (!c->pub_host) return DSX_OK;
+  StitchArgs ta{};
+  ta.state = c->state.p;
+  ta.host_state = c->pub_host;
+  ta.seq = c->pub_seq;
+  c->pub_host = nullptr;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, c->stream, ta);
+  HIPCHK(c, hipGetLastError());
   return DSX_OK;
 }
 
@@ -866,6 +892,11 @@ int ensure_attr_walk(dsx_ctx* c) {
 }
 
 int flush_behind(dsx_ctx* c) {
+  const int rc = flush_tasks(c);
+  return rc ? rc : flush_publish(c);
+}
+
+int flush_tasks(dsx_ctx* c) {
   if (c->behind.empty()) return DSX_OK;
   HIPCHK(c, hipSetDevice(c->device));
   // round 1: the walked call's finish and the other's walk (independent);
@@ -961,10 +992,14 @@ extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
         break;
       }
   }
-  if (q.done) {
-    HIPCHK(c, hipEventSynchronize(q.done));
-  } else {
-    // poll the published seq; the stream going idle without it is an error
+  if (c->pub_host && c->pub_seq == q.seq) {  // no later scan carried its publish
+    const int rc = flush_publish(c);
+    if (rc) return rc;
+  }
+  if (q.done) HIPCHK(c, hipEventSynchronize(q.done));
+  {
+    // poll the published seq (published after the event when a later scan
+    // or flush_publish carries it); the stream going idle without it is an error
     const volatile uint64_t* sp = &c->h_ring[q.slot].seq;
     for (uint32_t spins = 1; *sp != q.seq; ++spins) {
       if (spins % 4096u == 0) {
@@ -1020,7 +1055,11 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
   const bool queued = (flags & DSX_NO_SYNC) && dev_out;
   const bool fuse = queued && behind_ok(c, d_blob, len, p);
   if (!fuse) {  // every other call starts after the stitches still behind
-    rc = flush_behind(c);
+    rc = flush_tasks(c);
+    if (rc) return rc;
+  }
+  if (!queued) {  // (a queued call's first scan publishes the previous one's state)
+    rc = flush_publish(c);
     if (rc) return rc;
   }
   if (queued) {
@@ -1045,7 +1084,9 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
     const bool timed = (flags & DSX_TIMED) != 0;
     c->timing = timed;
     if (timed) std::swap(c->pev, c->q_pev[q.slot]);
+    c->defer_publish = true;
     rc = run_device(c, (const uint8_t*)d_blob, len, cc);
+    c->defer_publish = false;
     if (timed) std::swap(c->pev, c->q_pev[q.slot]);
     q.npiece = timed ? c->npiece_call : 0u;
     c->timing = true;

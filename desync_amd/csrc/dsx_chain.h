@@ -11,6 +11,24 @@ namespace dsx {
 
 constexpr uint64_t kNone = ~0ull;
 
+// A piece's chain state into its pinned host slot, seq last once the field
+// stores are complete (the slot is uncached host memory: a store completes
+// when it is performed there), so a host that polls seq (queued calls,
+// dsx_result) reads this piece's fields.  Called after the piece's stitch
+// has ended (publish_kernel, or the next scan's block 0), so its cut list
+// is complete too.  (A system-scope fence here also wrote back and
+// invalidated the L2: 4.3 us per piece.)
+__device__ __forceinline__ void publish_state(volatile HostState* h, const DevState* st,
+                                              uint64_t seq) {
+  h->carry = st->carry;
+  h->total = st->total;
+  h->repaired = st->repaired;
+  h->done = st->done;
+  h->err = st->err;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  h->seq = seq;
+}
+
 // The same source searched by a whole wavefront: 64 candidates per LDS read
 // and a ballot, so a chain step costs one LDS round trip instead of one per
 // candidate passed (the walks are latency-bound: one chain per wave).

@@ -43,7 +43,9 @@ struct TestConsts {
   uint32_t vmax1;  // MODE 2, scanl: vmax + 1 (candidate => t + 1 < vmax1; d >= 3 keeps it < 2^32)
 };
 
-struct TaskArgs;  // dsx_stitch.h
+struct TaskArgs;   // dsx_stitch.h
+struct DevState;   // dsx_stitch.h
+struct HostState;  // dsx_stitch.h
 
 struct ScanArgs {
   const uint8_t* base;   // device pointer of the piece's first byte
@@ -78,6 +80,12 @@ struct ScanArgs {
   // scanl_kernel<FUSE>: the stitch tasks it carries, in pinned host memory
   // (read once per task; by value they held ~90 more SGPRs through the scan)
   const TaskArgs* tasks;
+  // the previous queued piece's chain state, published by block 0 at the
+  // start of this scan (a kernel boundary after that piece's stitch) instead
+  // of by a publish_kernel of its own (pub_host null: nothing to publish)
+  const DevState* pub_state;
+  HostState* pub_host;
+  uint64_t pub_seq;
 };
 
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches

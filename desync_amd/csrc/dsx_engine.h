@@ -34,6 +34,7 @@ template <int PER>
 __global__ void finish_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);
 __global__ void publish_kernel(StitchArgs a);
+__global__ void noop_kernel();
 __global__ void state_init_kernel(DevState* st, uint64_t carry);
 __global__ void gen_uniform_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed);
 __global__ void gen_dedup_kernel(uint8_t* dst, uint64_t offset, uint64_t len, uint64_t seed,
@@ -157,7 +158,12 @@ struct dsx_ctx {
   uint64_t last_region_bytes = 0;  // geometry of the last enqueued piece's region lists
   uint32_t last_nregions = 0, last_region_cap = 0;
   uint64_t init_carry = 0;
-  bool last_finish = false;  // the last stitch ended with publish_kernel (the host may poll)
+  bool last_finish = false;  // the last stitch publishes its state (the host may poll)
+  // a queued call's final state is published by the next scan's block 0
+  // (no publish_kernel of its own); flush_publish() launches it otherwise
+  bool defer_publish = false;       // set while a queued cut_device call is enqueued
+  HostState* pub_host = nullptr;    // pending: slot ...
+  uint64_t pub_seq = 0;             // ... and piece seq
   // stitch behind the scan (DSX_FUSE, default on): queued one-piece calls
   // whose walk (walked = false) or finish (walked = true) runs as tasks in
   // the next queued call's scan; flush_behind() launches them on their own
@@ -331,6 +337,8 @@ int ensure_attr_walk(dsx_ctx* c);
 // launch the stitch tasks of the queued calls still behind (before any other
 // work on the context, and when such a call is collected)
 int flush_behind(dsx_ctx* c);
+int flush_tasks(dsx_ctx* c);    // flush_behind without the pending publish
+int flush_publish(dsx_ctx* c);  // launch the pending publish, if any
 #define DSX_FLUSH_BEHIND(c)                  \
   do {                                       \
     if (c) {                                 \

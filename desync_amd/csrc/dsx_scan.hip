@@ -345,6 +345,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
 
   if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.pub_host)  // the previous piece's state
+    publish_state(a.pub_host, a.pub_state, a.pub_seq);
   if (blockIdx.x == 0 && threadIdx.x == 8) {  // the task counters of the next slot
     a.queue_next[1] = 0u;
     a.queue_next[2] = 0u;
@@ -649,6 +651,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
                                         : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
 
   if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.pub_host)  // the previous piece's state
+    publish_state(a.pub_host, a.pub_state, a.pub_seq);
   if (blockIdx.x == 0 && threadIdx.x == 8) {  // the task counters of the next slot
     a.queue_next[1] = 0u;
     a.queue_next[2] = 0u;

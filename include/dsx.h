@@ -111,9 +111,15 @@ int dsx_progress(dsx_ctx_t *ctx, uint64_t *bytes);
                              queued calls record none (an event costs ~6 us of stream time) */
 
 /* Device-resident blob (HBM) -> cut list.  d_blob must stay valid until the
- * call (or, with DSX_NO_SYNC, dsx_sync()) returns.  If cap is too small the
- * call returns DSX_E_CAPACITY and *n_out holds the required count (an upper
- * bound of len/min + 2 always suffices). */
+ * call (with DSX_NO_SYNC: its dsx_result()) returns -- a queued call that
+ * needs the general path (dense candidates, a stitch repair) is re-run from
+ * the blob inside dsx_result().  If cap is too small the call returns
+ * DSX_E_CAPACITY and *n_out holds the required count (an upper bound of
+ * len/min + 2 always suffices).  A queued call's stitch publishes its state
+ * into pinned host memory and dsx_result() polls it (no event per call);
+ * with the environment variable DSX_FUSE=1 (off by default) the stitch of a
+ * queued one-piece call runs as tasks inside the next queued calls' scans
+ * and is completed by dsx_result() when no later call carries it. */
 int dsx_cut_device(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, const dsx_params_t *p,
                    uint64_t *out_ends, uint64_t cap, uint64_t *n_out, uint32_t flags);
 int dsx_sync(dsx_ctx_t *ctx);
