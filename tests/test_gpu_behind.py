@@ -116,10 +116,17 @@ def test_behind_sequence(fctx):
             q.collect()
 
 
-def test_behind_interleaved_sync_calls(fctx):
-    """A synchronous call and a chunk-ID call between queued ones run after
-    the stitches still behind, and every result stays exact."""
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_behind_interleaved_sync_calls(monkeypatch, fuse):
+    """A synchronous call, a chunk-ID call and a host-memory call between
+    queued ones run after the stitches still behind (DSX_FUSE=1) and after
+    the queued calls' pending publish (the next scan publishes a queued call's
+    state, or flush_publish), and every result stays exact; a timed queued
+    call (its own events) mixes in."""
     import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_FUSE", fuse)
+    fctx = _lib.Context(0)
     b = _blobs()
     q = Queue(fctx)
     q.submit(b["u40"])
@@ -130,9 +137,16 @@ def test_behind_interleaved_sync_calls(fctx):
     q.submit(b["zeros"])
     ids = desync_amd.chunk_ids(ptr, b["u300"].size, got[:50], 0, ctx=fctx)
     assert len(ids) == 50
-    q.submit(b["u1"])
+    q.submit(b["u1"], flags=_lib.DSX_TIMED)
+    q.submit(b["u40"])
+    q.collect()  # (the oldest: published by a later scan)
+    assert np.array_equal(desync_amd.cut_host(b["u1"], MIN, AVG, MAX, ctx=fctx),
+                          o.chunk_stream(b["u1"], MIN, AVG, MAX))
     while q.pending:
         q.collect()
+    q.submit(b["u1"])  # the last queued call: collected with no scan after it
+    q.collect()
+    fctx.close()
 
 
 def test_behind_redo_on_suspect_segments(monkeypatch):
