@@ -96,7 +96,7 @@ class Seam(ctypes.Structure):
 
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()  # (re-entrant: a Chunker's __del__ may return its context to the pool)
 
 
 def _share_torch_hip_runtime():
@@ -237,7 +237,7 @@ class Context:
 
 
 _default = {}
-_pool = {}  # device -> idle contexts (IndexFromFile is re-entrant, a context is not)
+_pool = {}  # (device, DSX_* env) -> idle contexts (IndexFromFile is re-entrant, a context is not)
 
 
 def default_context(device=0):
@@ -246,6 +246,47 @@ def default_context(device=0):
         ctx = Context(device)
         _default[device] = ctx
     return ctx
+
+
+_POOL_IDLE = 4  # idle contexts kept per device (each holds its pipeline buffers)
+
+
+def _env_key(device):
+    # a context reads its DSX_* settings from the environment when created:
+    # it is handed out again only under the same settings
+    return (device, tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("DSX_"))))
+
+
+def acquire_context(device=0):
+    """A context no other thread uses until release_context(): an idle pooled
+    one (its pinned and device buffers already sized by earlier calls) or a
+    new one.  A new context costs ~0.2 s of allocations once its pipelines
+    run; a pooled one costs nothing."""
+    key = _env_key(device)
+    ctx = None
+    with _lock:
+        idle = _pool.setdefault(key, [])
+        while idle and ctx is None:
+            ctx = idle.pop()
+            ctx = ctx if ctx.h else None  # (closed meanwhile: reset_context_pool)
+    if ctx is None:
+        ctx = Context(device)
+        ctx._pool_key = key
+    return ctx
+
+
+def release_context(ctx):
+    """Returns a context from acquire_context() to its pool (closed instead
+    when the pool is full or the context is closed)."""
+    if ctx is None or not ctx.h:
+        return
+    key = getattr(ctx, "_pool_key", None) or _env_key(ctx.device)
+    with _lock:
+        idle = _pool.setdefault(key, [])
+        if len(idle) < _POOL_IDLE:
+            idle.append(ctx)
+            return
+    ctx.close()
 
 
 class pooled_context:
@@ -258,16 +299,11 @@ class pooled_context:
         self.ctx = None
 
     def __enter__(self):
-        with _lock:
-            idle = _pool.setdefault(self.device, [])
-            self.ctx = idle.pop() if idle else None
-        if self.ctx is None:
-            self.ctx = Context(self.device)
+        self.ctx = acquire_context(self.device)
         return self.ctx
 
     def __exit__(self, *exc):
-        with _lock:
-            _pool.setdefault(self.device, []).append(self.ctx)
+        release_context(self.ctx)
         self.ctx = None
         return False
 

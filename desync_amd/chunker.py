@@ -23,6 +23,7 @@ buffer with readinto when the reader has it) and hands out confirmed chunks.
 from __future__ import annotations
 
 import ctypes
+import itertools
 
 from . import _lib
 from ._lib import check, lib
@@ -33,6 +34,7 @@ _READ = 8 << 20
 # confirmed chunks taken from the library per call (Next() then serves them
 # without a library call per chunk)
 _POP = 4096
+_tokens = itertools.count()
 
 
 class Params:
@@ -84,13 +86,26 @@ class Chunker:
         self._zero_copy = bool(zero_copy)
         self.r = reader
         # Like a Go Chunker (its own buffer and hash state, chunker.go:108-131)
-        # every Chunker owns a library context: the stream state and device
-        # scratch live there.  A caller-supplied ctx must not carry another
-        # unfinished stream (dsx_stream_begin refuses: DSX_E_STATE).
+        # every Chunker owns a library context while it lives: the stream
+        # state and device scratch live there.  Without a ctx it takes one
+        # from the per-device pool and returns it on close(), so the buffers
+        # sized by earlier streams are reused (a fresh context's allocations
+        # cost more than chunking 512 MiB).  A caller-supplied ctx must not
+        # carry another unfinished stream (dsx_stream_begin: DSX_E_STATE).
         self._own = ctx is None
-        self.ctx = _lib.Context(device) if ctx is None else ctx
-        check(lib().dsx_stream_begin(self.ctx.h, ctypes.byref(self.params.c)), self.ctx.h)
-        self.ctx._stream_owner = self  # (close() must not end a later Chunker's stream)
+        self.ctx = _lib.acquire_context(device) if ctx is None else ctx
+        try:
+            check(lib().dsx_stream_begin(self.ctx.h, ctypes.byref(self.params.c)), self.ctx.h)
+        except BaseException:
+            if self._own:  # (not pooled: it failed)
+                self.ctx.close()
+            self.ctx = None
+            raise
+        # (close() must not end a later Chunker's stream; a token, not self: a
+        # reference from the context back to this Chunker would make a cycle,
+        # and the cycle collector finalizes a pooled context with it)
+        self._token = next(_tokens)
+        self.ctx._stream_owner = self._token
         self._eof = False
         self._start = ctypes.c_uint64()
         self._size = ctypes.c_uint64()
@@ -111,6 +126,11 @@ class Chunker:
         self._n = ctypes.c_uint64()
         self._win, self._wbase = None, 0  # view of the library's held bytes
         self._last_id = None
+        # read-ahead beyond the reference's buffer (0: none).  A consumer that
+        # reads the stream to its end anyway (ChunkStream) sets it, so that the
+        # next batches are on the GPU while it works through this one's chunks
+        # instead of the read, the GPU and the consumer taking turns.
+        self._ra = 0
 
     # -- reference API -----------------------------------------------------
     def Next(self):
@@ -126,6 +146,10 @@ class Chunker:
             if self._err is not None and target > self._E:
                 return self._read_error()
             self._R = target
+        if self._ra and self._pos - self._cur < self._ra // 2:
+            target = self._cur + self._ra
+            while self._pos < target and not self._eof and self._err is None:
+                self._fill()
         if self._qi < len(self._q):
             return self._take()
         while True:
@@ -195,14 +219,20 @@ class Chunker:
         return self.params.max
 
     def close(self):
-        """Release the stream (and the context, if this Chunker created it)."""
-        if self.ctx is not None and self.ctx.h:
-            if getattr(self.ctx, "_stream_owner", None) is self:
-                lib().dsx_stream_end(self.ctx.h)
-                self.ctx._stream_owner = None
+        """Release the stream (and return the context to the pool, if this
+        Chunker took it from there; a context whose stream did not end
+        cleanly is closed instead)."""
+        ctx, self.ctx = self.ctx, None
+        if ctx is not None and ctx.h:
+            rc = 0
+            if getattr(ctx, "_stream_owner", None) == getattr(self, "_token", -1):
+                rc = lib().dsx_stream_end(ctx.h)
+                ctx._stream_owner = None
             if self._own:
-                self.ctx.close()
-        self.ctx = None
+                if rc == 0:
+                    _lib.release_context(ctx)
+                else:
+                    ctx.close()
 
     def __del__(self):
         try:

@@ -76,6 +76,7 @@ class MemoryStore:
 
 
 _BATCH = 64  # chunks per hand-off to the store workers
+_READ_AHEAD = 256 << 20  # two of dsx_stream_ids' 128 MiB batches
 
 
 def ChunkStream(ctx, c, ws, n):
@@ -86,6 +87,11 @@ def ChunkStream(ctx, c, ws, n):
     as the reference's select on ctx.Done() does (index.go:203-206).  A
     reader error (ChunkerReadError) or a store error is raised."""
     c.EnableIDs()
+    if hasattr(c, "_ra"):
+        # ChunkStream reads the stream to its end: the reader may run two ID
+        # batches (2 x 128 MiB) ahead, so batches are scanned and hashed while
+        # this thread hands out the chunks before them
+        c._ra = max(c._ra, _READ_AHEAD)
     storage = ChunkStorage(ws)
     chunks = []
     nw = max(1, int(n))

@@ -385,6 +385,42 @@ def test_chunk_stream_errors():
     assert [ch.Start + ch.Size for ch in idx.Chunks] == ref[:5].tolist()
 
 
+def test_chunker_context_pool(monkeypatch):
+    """A Chunker without a ctx takes an idle pooled context and returns it on
+    close(), mid-stream too; the next Chunker chunks correctly on it.  A
+    context made under other DSX_* settings is not handed out."""
+    import desync_amd
+    from desync_amd import _lib
+    _lib.reset_context_pool()
+    data = o.synth_uniform(48, 0, (24 << 20) + 5)
+    ref = o.chunk_stream(data, MIN, AVG, MAX).tolist()
+
+    def chunker():
+        return desync_amd.NewChunker(io.BytesIO(data.tobytes()), MIN, AVG, MAX)
+
+    try:
+        c1 = chunker()
+        h1 = c1.ctx.h.value
+        s, b = c1.Next()
+        assert s == 0 and len(b) == ref[0]
+        c1.close()  # mid-stream
+        c2 = chunker()
+        assert c2.ctx.h.value == h1
+        assert [s + len(b) for s, b in c2] == ref
+        c2.close()
+        monkeypatch.setenv("DSX_SCAN_NT", "0")
+        c3 = chunker()
+        assert c3.ctx.h.value != h1
+        assert [s + len(b) for s, b in c3] == ref
+        c3.close()
+        monkeypatch.delenv("DSX_SCAN_NT")
+        c4 = chunker()
+        assert c4.ctx.h.value == h1
+        c4.close()
+    finally:
+        _lib.reset_context_pool()
+
+
 # ------------------------------------------------- dsx_ids_fd / dsx_ids_host
 @pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
 def test_ids_fd_many_windows(tmp_path, monkeypatch, algo):
