@@ -265,10 +265,15 @@ def acquire_context(device=0):
     key = _env_key(device)
     ctx = None
     with _lock:
+        # idle contexts made under other settings are not handed out again
+        # while these hold: close them rather than keep their buffers
+        stale = [c for k in list(_pool) if k[0] == device and k != key for c in _pool.pop(k)]
         idle = _pool.setdefault(key, [])
         while idle and ctx is None:
             ctx = idle.pop()
             ctx = ctx if ctx.h else None  # (closed meanwhile: reset_context_pool)
+    for c in stale:
+        c.close()
     if ctx is None:
         ctx = Context(device)
         ctx._pool_key = key

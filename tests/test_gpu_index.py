@@ -388,7 +388,8 @@ def test_chunk_stream_errors():
 def test_chunker_context_pool(monkeypatch):
     """A Chunker without a ctx takes an idle pooled context and returns it on
     close(), mid-stream too; the next Chunker chunks correctly on it.  A
-    context made under other DSX_* settings is not handed out."""
+    context made under other DSX_* settings is not handed out (and is closed
+    once a context is asked for under the new ones)."""
     import desync_amd
     from desync_amd import _lib
     _lib.reset_context_pool()
@@ -400,22 +401,27 @@ def test_chunker_context_pool(monkeypatch):
 
     try:
         c1 = chunker()
-        h1 = c1.ctx.h.value
+        x1 = c1.ctx
         s, b = c1.Next()
         assert s == 0 and len(b) == ref[0]
         c1.close()  # mid-stream
         c2 = chunker()
-        assert c2.ctx.h.value == h1
+        assert c2.ctx is x1
         assert [s + len(b) for s, b in c2] == ref
         c2.close()
         monkeypatch.setenv("DSX_SCAN_NT", "0")
         c3 = chunker()
-        assert c3.ctx.h.value != h1
+        x3 = c3.ctx
+        assert x3 is not x1 and not x1.h  # (the idle one, made under other settings, closed)
         assert [s + len(b) for s, b in c3] == ref
         c3.close()
+        c5 = chunker()
+        assert c5.ctx is x3
+        c5.close()
         monkeypatch.delenv("DSX_SCAN_NT")
         c4 = chunker()
-        assert c4.ctx.h.value == h1
+        assert c4.ctx is not x3 and not x3.h
+        assert [s + len(b) for s, b in c4] == ref
         c4.close()
     finally:
         _lib.reset_context_pool()
