@@ -139,3 +139,52 @@ def test_chop_batches():
     assert [c for _, b in got for c in b] == chunks
     for _, b in got:
         assert len(b) == 1 or b[-1].Start + b[-1].Size - b[0].Start <= chop._BATCH
+
+
+def test_context_pool(monkeypatch):
+    """_lib.acquire_context / release_context without a GPU (a stand-in
+    Context): an idle context is handed out again under the same DSX_*
+    settings only, stale ones are closed on the next acquire, at most
+    _POOL_IDLE stay idle, and a context closed while idle is skipped."""
+    from desync_amd import _lib
+
+    made = []
+
+    class FakeCtx:
+        def __init__(self, device=0):
+            self.h, self.device = object(), device
+            made.append(self)
+
+        def close(self):
+            self.h = None
+
+    monkeypatch.setattr(_lib, "Context", FakeCtx)
+    monkeypatch.setattr(_lib, "_pool", {})
+    for k in [k for k in os.environ if k.startswith("DSX_")]:
+        monkeypatch.delenv(k)
+    a = _lib.acquire_context(0)
+    _lib.release_context(a)
+    assert _lib.acquire_context(0) is a
+    b = _lib.acquire_context(0)  # a is in use: a new one
+    assert b is not a
+    _lib.release_context(a)
+    _lib.release_context(b)
+    with _lib.pooled_context(0) as c:
+        assert c in (a, b)
+    monkeypatch.setenv("DSX_SCAN_NT", "0")
+    d = _lib.acquire_context(0)
+    assert d not in (a, b) and a.h is None and b.h is None  # stale ones closed
+    _lib.release_context(d)
+    e = _lib.acquire_context(1)  # another device's pool does not touch device 0's
+    assert e is not d and d.h is not None
+    _lib.release_context(e)
+    many = [_lib.acquire_context(0) for _ in range(_lib._POOL_IDLE + 2)]
+    for x in many:
+        _lib.release_context(x)
+    assert sum(x.h is not None for x in many) == _lib._POOL_IDLE
+    idle = [x for x in many if x.h is not None]
+    for x in idle[:-1]:
+        x.close()  # closed while idle (reset_context_pool, another owner)
+    assert _lib.acquire_context(0) is idle[-1]
+    n = len(made)
+    assert _lib.acquire_context(0) not in many and len(made) == n + 1
