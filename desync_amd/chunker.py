@@ -136,8 +136,6 @@ class Chunker:
     def Next(self):
         """(start, chunk bytes); (start, empty) when the stream is exhausted.
         With zero_copy the chunk is a view valid until the next call."""
-        L = lib()
-        h = self.ctx.h
         mx = self.params.max
         if self._R - self._cur < mx:  # the reference's fillBuffer
             target = self._cur + 10 * mx
@@ -152,6 +150,7 @@ class Chunker:
                 self._fill()
         if self._qi < len(self._q):
             return self._take()
+        L, h = lib(), self.ctx.h
         while True:
             rc = check(L.dsx_stream_pop_many(h, self._ends, self._idbuf, _POP, ctypes.byref(self._start),
                                              ctypes.byref(self._n)), h)
