@@ -1,18 +1,26 @@
 #!/usr/bin/env python3
 """Benchmark: GiB/s chunked (device-resident blob -> cut list), BASELINE.json.
 
-Workload (BASELINE.json configs[1]): a 1 GiB synthetic uniform blob (splitmix64,
-seed 1, generated on device) chunked with desync's default min/avg/max =
-16/64/256 KiB; the blob is in HBM when the timed region starts and one step
-produces the complete cut list in HBM (scan + stitch, libdsx.so).
+Workload (default): BASELINE config 5's per-GPU shard -- 32 GiB of the seed-3
+splitmix64 uniform blob per GPU (256 GiB over 8 GPUs), generated on device and
+chunked with desync's default min/avg/max = 16/64/256 KiB.  The blob is in HBM
+when the timed region starts and one step produces the complete cut list of
+the shard in HBM (scan + stitch of four 8 GiB pieces, libdsx.so).  The same
+per-GPU shape runs at every N (weak scaling), so the N = 1 line and the
+1/2/4/8-GPU curve are one configuration.  --config2 runs BASELINE config 2's
+shape instead (1 GiB, seed 1).
 
 N > 1 (one process per GPU, torch.distributed over RCCL): rank r holds bytes
-[r GiB, (r+1) GiB) of an N GiB blob (+64 B halo, regenerated locally; 32 GiB
-of the seed-3 blob per rank with --config5), chunks it speculatively
-(dsx_shard_local), all-gathers the small seam records (RCCL, in place in
-HBM), and resolves its final cut list in HBM (dsx_shard_resolve_async) --
-weak scaling.  The whole step is ordered on the library stream; the host
-waits once per step (dsx_shard_collect).
+[r*n, (r+1)*n) of the N*n-byte blob (+64 B halo, regenerated locally), chunks
+it speculatively (dsx_shard_local), all-gathers the small seam records (RCCL,
+in place in HBM), and resolves its final cut list in HBM
+(dsx_shard_resolve_async).  The whole step is ordered on the library stream;
+the host waits once per step (dsx_shard_collect).
+
+roofline.kernel_ms is the mean duration of the scan launches of exactly the
+timed jobs, stamped from inside the kernel (dsx_stamps_begin/end:
+s_memrealtime at the first wave's first and the last wave's last
+instruction), with nothing added between the launches.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -33,25 +41,27 @@ sys.path.insert(0, REPO)
 GiB = 1 << 30
 MIN, AVG, MAX = 16 * 1024, 64 * 1024, 256 * 1024
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+PIECE = 8 * GiB          # bytes per scan launch (the engine's piece, kPieceMax)
+CPU_SAMPLE = GiB         # cpu_baseline: the first GiB of the shard
 METRIC = "GiB/s chunked (device-resident blob→cut list), 16/64/256KiB, 1/2/4/8 MI355X"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: the timed jobs run in the chip's steady state.  The first
-    # ~15 ms of back-to-back scans after an idle period run ~15 % slower (a
-    # power-management transient: the scan holds the board at its 1400 W cap,
-    # DESIGN.md 7); 100 warm-up jobs (~25 ms) pass it, 400 timed jobs ~0.1 s.
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--gib", type=float, default=1.0, help="GiB per GPU")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--gib", type=float, default=None,
+                    help="GiB per GPU (default: the workload's BASELINE config: 32 uniform "
+                         "(config 5 shard), 16 dedup (config 3), 64 zeros (config 4))")
     ap.add_argument("--workload", default="uniform", choices=["uniform", "dedup", "zeros"])
     ap.add_argument("--seed", type=int, default=0,
-                    help="generator seed (0: 1 for uniform, 2 for dedup)")
+                    help="generator seed (0: 3 for uniform -- config 5 --, 2 for dedup)")
     ap.add_argument("--config5", action="store_true",
-                    help="BASELINE config 5's shard shape: 32 GiB of the seed-3 uniform blob "
-                         "per GPU (256 GiB over 8 GPUs)")
+                    help="BASELINE config 5's shard shape (the default): 32 GiB of the seed-3 "
+                         "uniform blob per GPU (256 GiB over 8 GPUs)")
+    ap.add_argument("--config2", action="store_true",
+                    help="BASELINE config 2's shape: 1 GiB of the seed-1 uniform blob per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the cpu_baseline leg (0: the job's CPU share)")
@@ -63,10 +73,18 @@ def parse():
                     help="N>1: compare the concatenated per-rank cut lists with one "
                          "dsx_cut_device over the whole blob on rank 0 (small sizes)")
     args = ap.parse_args()
-    if args.config5:
-        args.gib, args.workload, args.seed = 32.0, "uniform", 3
+    if args.config2:
+        args.workload, args.gib, args.seed = "uniform", args.gib or 1.0, args.seed or 1
+    elif args.config5:
+        args.workload = "uniform"
+    if args.gib is None:
+        args.gib = {"uniform": 32.0, "dedup": 16.0, "zeros": 64.0}[args.workload]
     if not args.seed:
-        args.seed = 2 if args.workload == "dedup" else 1
+        args.seed = 2 if args.workload == "dedup" else 3
+    args.config = ("config 5 shard" if (args.workload, args.gib, args.seed) == ("uniform", 32.0, 3)
+                   else "config 2" if (args.workload, args.gib, args.seed) == ("uniform", 1.0, 1)
+                   else "config 3" if (args.workload, args.gib) == ("dedup", 16.0)
+                   else "config 4" if (args.workload, args.gib) == ("zeros", 64.0) else None)
     if args.inflight <= 0:
         args.inflight = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
     return args
@@ -90,17 +108,18 @@ def make_blob(ctx, t, offset, n, workload, seed):
 
 
 def load_traffic(workload, nbytes):
-    """HBM bytes per scan launch from the committed rocprofv3 PMC pass
-    (profiles/traffic_<workload>.json: L2 -> fabric read requests x their
+    """HBM bytes per scan launch of `nbytes` from the committed rocprofv3 PMC
+    pass (profiles/traffic_<workload>_<nbytes>.json, or the older
+    profiles/traffic_<workload>.json: L2 -> fabric read requests x their
     sizes, tools/traffic_json.py)."""
-    path = os.path.join(REPO, "profiles", f"traffic_{workload}.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if int(d.get("bytes", -1)) == int(nbytes):
-            return float(d["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
-        pass
+    for name in (f"traffic_{workload}_{int(nbytes)}.json", f"traffic_{workload}.json"):
+        try:
+            with open(os.path.join(REPO, "profiles", name)) as f:
+                d = json.load(f)
+            if int(d.get("bytes", -1)) == int(nbytes):
+                return float(d["hbm_bytes_per_launch"])
+        except (OSError, ValueError, KeyError):
+            pass
     return None
 
 
@@ -217,7 +236,6 @@ def main():
     make_blob(ctx, blob, rank * n - halo, n + halo, args.workload, args.seed)
     d_ptr = blob.data_ptr() + halo
     cap = n // MIN + 4
-    out = torch.empty(cap, dtype=torch.int64, device="cuda")
     shard = None
     lanes = []
     if world > 1:
@@ -238,14 +256,10 @@ def main():
     # queued on the context (DSX_NO_SYNC): job s is enqueued before the host
     # waits for job s - inflight, so the GPU is not idle while the host wakes
     # up.  Each job's stitch follows its scan on the library stream; the host
-    # polls the state the stitch publishes (no event between jobs).  With
-    # DSX_FUSE=1 a queued job's stitch runs as tasks inside the next two jobs'
-    # scans instead (throughput-neutral under the power cap).
+    # polls the state the stitch publishes (no event between jobs).
     depth = min(8, max(1, args.inflight)) if world == 1 else 1
     outs = [torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(depth)]
     queued = []
-    scan_ms = []
-    stitch_ms = []
     cnt = ctypes.c_uint64()
 
     def collect():
@@ -253,7 +267,7 @@ def main():
         queued.pop(0)
         return cnt.value
 
-    def step(s, record=False):
+    def step(s):
         if world == 1:
             got = collect() if len(queued) == depth else None
             _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
@@ -266,7 +280,7 @@ def main():
         # records in HBM, resolve the seams (desync_amd/shard.py)
         return shard.run()
 
-    def drain(nsteps, record):
+    def drain():
         last = None
         while queued:
             last = collect()
@@ -291,27 +305,30 @@ def main():
     if world == 1:
         for s in range(args.warmup):
             step(s)
-        drain(args.warmup, False)
+        drain()
     else:
         for ln in lanes:  # every lane once, in order on every rank
             ln.run()
         run_lanes(args.warmup)
     torch.cuda.synchronize()
+    if world == 1:  # in-kernel stamps of exactly the timed jobs' scan launches
+        ctx.stamps_begin(args.steps * ((n + PIECE - 1) // PIECE) + 8)
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
     chunks = 0
     if world == 1:
         for s in range(args.steps):
-            r = step(s, record=True)
+            r = step(s)
             chunks = r if r is not None else chunks
-        chunks = drain(args.steps, True)
+        chunks = drain()
     else:
         chunks = run_lanes(args.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    stamps = ctx.stamps_end() if world == 1 else []
     if dist:
         tdev = "cuda" if backend == "nccl" else "cpu"
         tt = torch.tensor([dt], dtype=torch.float64, device=tdev)
@@ -322,37 +339,6 @@ def main():
         chunks = int(tc.item())
     ms_per_step = dt / args.steps * 1000.0
     value = (n * world * args.steps) / dt / GiB
-
-    # roofline timing: with jobs in flight a scan's HIP events also bracket
-    # the other contexts' kernels, so the per-launch scan duration comes from
-    # HIP events on the library stream in a pass of the same jobs queued
-    # back to back on one context (DSX_NO_SYNC | DSX_TIMED): no other stream's
-    # kernels in between and, unlike a call-and-wait loop, no idle GPU between
-    # jobs (after a host round trip of idle the scan ran up to 15 % slower)
-    if world == 1:
-        scan_ms.clear()
-        stitch_ms.clear()
-        tdepth = 0
-
-        def collect_timed():
-            _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
-            assert cnt.value == chunks, "timing pass disagrees with the timed jobs"
-            st = ctx.stats()
-            scan_ms.append(st.scan_ms)
-            stitch_ms.append(st.stitch_ms)
-
-        for _ in range(args.steps):
-            if tdepth == 4:
-                collect_timed()
-                tdepth -= 1
-            _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(d_ptr), n, ctypes.byref(p.c),
-                                        ctypes.c_void_p(out.data_ptr()), cap, ctypes.byref(cnt),
-                                        _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC | _lib.DSX_TIMED),
-                       ctx.h)
-            tdepth += 1
-        while tdepth:
-            collect_timed()
-            tdepth -= 1
 
     if args.check and world > 1:
         mine = torch.from_numpy(shard.cuts().astype(np.int64))
@@ -381,18 +367,23 @@ def main():
             "data": f"synthetic ({DATA_LABEL[args.workload].format(seed=args.seed)}, generated on device)",
             "config": {
                 "workload": (f"{args.gib:g} GiB {args.workload} blob per GPU"
-                             f"{' (BASELINE config 5 shard shape)' if args.config5 else ''}, desync make "
-                             f"min/avg/max 16/64/256 KiB, device-resident blob -> cut list in HBM"),
+                             f"{' (BASELINE ' + args.config + ' shape)' if args.config else ''}, "
+                             f"desync make min/avg/max 16/64/256 KiB, device-resident blob -> "
+                             f"cut list in HBM"),
                 "bytes_per_gpu": n,
                 "chunks": int(chunks),
                 "parallelism": f"range-shard x{world}" if world > 1 else "single GPU",
                 "jobs_in_flight": depth if world == 1 else len(lanes),
             },
         }
-        if world == 1 and scan_ms:
-            avg_scan = float(np.mean(scan_ms))
-            achieved = n / (avg_scan / 1e3) / 1e9
-            traffic = load_traffic(args.workload, n)
+        if world == 1 and stamps:
+            dur = np.array([st.ms for st in stamps])
+            nb = np.array([st.bytes for st in stamps], dtype=np.float64)
+            cyc = sum(st.wave_cycles for st in stamps)
+            tick = sum(st.wave_ticks for st in stamps)
+            per_launch = int(np.median(nb))
+            achieved = float(nb.sum() / (dur.sum() / 1e3) / 1e9)
+            traffic = load_traffic(args.workload, per_launch)
             res["roofline"] = {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -401,11 +392,17 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": "dsx::scanl_kernel",
-                "kernel_ms": round(avg_scan, 4),
-                "stitch_ms": round(float(np.mean(stitch_ms)), 4),
+                "bytes_per_launch": per_launch,
+                "launches": len(stamps),
+                "kernel_ms": round(float(dur.mean()), 4),
+                "kernel_ms_min_max": [round(float(dur.min()), 4), round(float(dur.max()), 4)],
+                "clock_mhz": round(100.0 * cyc / tick, 1) if tick else None,
+                "scan_share_of_step": round(float(dur.sum()) / (dt * 1e3), 4),
+                "timing": "in-kernel s_memrealtime stamps of the timed jobs' scan launches",
             }
         if world == 1 and not args.no_cpu:
-            host = blob[halo:].cpu().numpy()
+            # a bounded sample: the shard's first GiB (the leg is ~10-30 s of CPU work)
+            host = blob[halo:halo + min(n, CPU_SAMPLE)].cpu().numpy()
             res["cpu_baseline"] = cpu_baseline(host, args.cpu_threads or None)
         print(json.dumps(res), flush=True)
     if dist:

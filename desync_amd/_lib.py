@@ -57,7 +57,7 @@ EXPORTS = (
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host", "dsx_copy",
     "dsx_ids_fd", "dsx_ids_host", "dsx_progress", "dsx_shard_resolve_async", "dsx_shard_collect",
-    "dsx_ctx_stream",
+    "dsx_ctx_stream", "dsx_stamps_begin", "dsx_stamps_end",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -81,6 +81,21 @@ class Stats(ctypes.Structure):
         ("repaired_segments", ctypes.c_uint64), ("dense_fallbacks", ctypes.c_uint64),
         ("scan_ms", ctypes.c_float), ("stitch_ms", ctypes.c_float),
     ]
+
+
+class ScanStamp(ctypes.Structure):
+    """dsx_scan_stamp_t: one scan launch timed from inside the kernel."""
+
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("seq", "bytes", "t_first", "t_last", "wave_cycles", "wave_ticks", "waves", "reserved")]
+
+    @property
+    def ms(self):
+        return (self.t_last - self.t_first) / 1e5  # s_memrealtime: 100 MHz
+
+    @property
+    def mhz(self):
+        return 100.0 * self.wave_cycles / self.wave_ticks if self.wave_ticks else 0.0
 
 
 class Seam(ctypes.Structure):
@@ -124,12 +139,13 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                 "(make -C desync_amd/csrc). desync_amd has no CPU fallback.")
-        diag_env = [k for k in ("DSX_SCAN_VARIANT", "DSX_SCAN_CFG")
+        diag_env = [k for k in ("DSX_SCAN_VARIANT", "DSX_SCAN_CFG", "DSX_FUSE")
                     if os.environ.get(k, "0") not in ("", "0")]
         if diag_env and not os.path.basename(LIB_PATH).startswith("libdsx_diag"):
             raise ImportError(
-                f"{', '.join(diag_env)} selects a diagnostic scan kernel, which only the "
-                "diagnostic build holds: make -C desync_amd/csrc diag and set "
+                f"{', '.join(diag_env)} selects a diagnostic kernel path (scan ablations, "
+                "other geometries, the stitch behind the scan), which only the diagnostic "
+                "build holds: make -C desync_amd/csrc diag and set "
                 "DSX_LIB_PATH=desync_amd/libdsx_diag.so")
         _share_torch_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
@@ -180,6 +196,8 @@ def lib():
             "dsx_debug_trace": (i32, [vp, vp, u64, P(u64), P(u64)]),
             "dsx_ids_fd": (i32, [vp, i32, u64, u64, u64, vp, u64, i32, vp]),
             "dsx_ids_host": (i32, [vp, vp, u64, u64, vp, u64, i32, vp]),
+            "dsx_stamps_begin": (i32, [vp, u64]),
+            "dsx_stamps_end": (i32, [vp, vp, u64, P(u64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -234,6 +252,19 @@ class Context:
         s = Stats()
         check(lib().dsx_get_stats(self.h, ctypes.byref(s)), self.h)
         return s
+
+    def stamps_begin(self, max_launches):
+        """Time the next max_launches scan launches from inside the kernel."""
+        check(lib().dsx_stamps_begin(self.h, int(max_launches)), self.h)
+        self._stamp_cap = int(max_launches)
+
+    def stamps_end(self):
+        """The stamped launches' ScanStamp records, in launch order."""
+        cap = getattr(self, "_stamp_cap", 0)
+        buf = (ScanStamp * max(1, cap))()
+        n = ctypes.c_uint64()
+        check(lib().dsx_stamps_end(self.h, buf, cap, ctypes.byref(n)), self.h)
+        return list(buf[:min(cap, n.value)])
 
 
 _default = {}

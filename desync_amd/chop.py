@@ -27,7 +27,7 @@ import threading
 import numpy as np
 
 from .errors import ChunkInvalid
-from .make import NullProgressBar, _contiguous_runs, file_size, ids_host
+from .make import NullProgressBar, _chunk_runs, file_size, ids_host
 from .stream import Chunk, ChunkStorage
 
 
@@ -40,7 +40,7 @@ def _batches(chunks, size):
     short at its end.  Chunks of a hand-built list need not be contiguous:
     each contiguous run is batched on its own."""
     i = 0
-    for run in _contiguous_runs(chunks):
+    for run in _chunk_runs(chunks):
         j = 0
         while j < len(run):
             k = j + 1

@@ -175,6 +175,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
 #endif
   if (const char* v = getenv("DSX_DIGEST_PC")) c->digest_pc = atoi(v);
   if (const char* v = getenv("DSX_DIGEST_PC_CHUNKS")) c->digest_pc_chunks = std::max(1, atoi(v));
+  if (const char* v = getenv("DSX_DIGEST_LPT")) c->digest_lpt = atoi(v) != 0;
   if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
@@ -186,7 +187,9 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SCAN_NT")) c->scan_nt = atoi(v) & 3;
   if (const char* v = getenv("DSX_FIXUP_FAST")) c->fixup_fast = atoi(v) != 0;
   if (const char* v = getenv("DSX_FINISH")) c->finish = atoi(v) != 0;
+#if DSX_DIAG  // the stitch behind the scan (tasks inside later scans): libdsx_diag.so only
   if (const char* v = getenv("DSX_FUSE")) c->fuse = atoi(v) != 0;
+#endif
 
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
@@ -237,7 +240,9 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   for (uint32_t i = 0; i < kQueueDepth; ++i)
     CREATE_STEP(hipEventCreateWithFlags(&c->q_ev[i], hipEventDisableTiming));
   CREATE_STEP(hipHostMalloc((void**)&c->h_res, 4 * sizeof(uint64_t)));
+#if DSX_DIAG
   CREATE_STEP(hipHostMalloc((void**)&c->h_tasks, dsx_ctx::kTaskRing * sizeof(TaskArgs), hipHostMallocCoherent));
+#endif
   memset(c->h_state, 0, sizeof(HostState));
   CREATE_STEP(c->state.ensure(1));
   // [0..1] overflow (piece parity); [32 + 256*parity + 32*x] the scan's work
@@ -260,6 +265,7 @@ extern "C" int dsx_ctx_destroy(dsx_ctx_t* c) {
   c->region_cnt2.release(); c->region_list2.release();
   c->flag_list.release(); c->lane_slot.release(); c->seg_info.release(); c->stage.release();
   c->dg_ends.release(); c->dg_ids.release(); c->dg_queue.release();
+  c->dg_order.release(); c->dg_cls.release();
   c->rep.release(); c->out_off.release(); c->out.release(); c->state.release();
   c->seg_info2.release(); c->stage2.release(); c->spec.release(); c->spec2.release();
   release_kept(c);
@@ -345,6 +351,57 @@ extern "C" int dsx_copy(dsx_ctx_t* c, void* dst, const void* src, uint64_t n) {
 extern "C" int dsx_get_stats(dsx_ctx_t* c, dsx_stats_t* out) {
   if (!c || !out) return DSX_E_INVAL;
   *out = c->stats;
+  return DSX_OK;
+}
+
+// In-kernel stamps of the next max_launches line-scan launches (bench.py's
+// roofline: the durations of exactly the launches its timed loop runs, with
+// no event between them).  Waits for the context's queued work first.
+extern "C" int dsx_stamps_begin(dsx_ctx_t* c, uint64_t max_launches) {
+  if (!c || max_launches == 0 || max_launches > (1ull << 24)) return DSX_E_INVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->scan_stream != c->stream) HIPCHK(c, hipStreamSynchronize(c->scan_stream));
+  HIPCHK(c, grow(c, c->stamp_ring, max_launches * kStampWords));
+  std::vector<uint64_t> init(max_launches * kStampWords, 0ull);
+  for (uint64_t i = 0; i < max_launches; ++i) init[i * kStampWords] = ~0ull;  // t_first: a minimum
+  HIPCHK(c, hipMemcpy(c->stamp_ring.p, init.data(), init.size() * sizeof(uint64_t),
+                      hipMemcpyHostToDevice));
+  c->stamp_meta.clear();
+  c->stamp_cap = max_launches;
+  c->stamping = true;
+  return DSX_OK;
+}
+
+// Stops stamping, waits for the stamped launches and copies min(cap, n)
+// records (in launch order) to out; *n = the launches stamped.
+extern "C" int dsx_stamps_end(dsx_ctx_t* c, dsx_scan_stamp_t* out, uint64_t cap, uint64_t* n) {
+  if (!c || !n || (cap && !out)) return DSX_E_INVAL;
+  const bool was = c->stamping;
+  c->stamping = false;
+  *n = 0;
+  if (!was) return DSX_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->scan_stream != c->stream) HIPCHK(c, hipStreamSynchronize(c->scan_stream));
+  const uint64_t k = c->stamp_meta.size();
+  *n = k;
+  const uint64_t m = std::min(cap, k);
+  if (!m) return DSX_OK;
+  std::vector<uint64_t> raw(m * kStampWords);
+  HIPCHK(c, hipMemcpy(raw.data(), c->stamp_ring.p, raw.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < m; ++i) {
+    const uint64_t* r = &raw[i * kStampWords];
+    dsx_scan_stamp_t s{};
+    s.seq = c->stamp_meta[i].first;
+    s.bytes = c->stamp_meta[i].second;
+    s.t_first = r[0];
+    s.t_last = r[1];
+    s.wave_cycles = r[2];
+    s.wave_ticks = r[3];
+    s.waves = r[4];
+    out[i] = s;
+  }
   return DSX_OK;
 }
 
@@ -482,6 +539,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   // of the calls behind it that this scan carries
   dsx_ctx::Behind me;
   TaskArgs tb{};
+#if DSX_DIAG
   if (cc.behind) {
     const bool second = (c->piece_seq + 1) % 2 == 1;
     const uint64_t seg = std::max<uint64_t>(c->seg_max_mult * p->max, c->seg_floor);
@@ -535,6 +593,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
       }
     }
   }
+#endif
   const uint64_t seq = ++c->piece_seq;
   const int par = (int)(seq & 1);
   hipStream_t ss = c->scan_stream;
@@ -572,13 +631,17 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   tb.counter = sa.queue + 1;  // (zeroed by the previous scan, with the queue)
   tb.farrive = sa.queue + 2;
 
+#if DSX_DIAG
   if (cc.behind) {
-    // the ring slot was last read by the scan kTaskRing pieces ago, which
-    // completed before any of the kQueueDepth queued calls still pending
-    TaskArgs* slot = c->h_tasks + (seq % dsx_ctx::kTaskRing);
+    // the ring advances with fused calls only: the slot was last read by the
+    // scan of the fused call kTaskRing (16) fused calls ago, which completed
+    // before the call kQueueDepth (8) queued calls ago was collected (a
+    // non-fused multi-piece call between them does not move the index)
+    TaskArgs* slot = c->h_tasks + (c->fuse_seq++ % dsx_ctx::kTaskRing);
     *slot = tb;
     sa.tasks = slot;
   }
+#endif
   if (line) {
     // region 0's descriptor: the warm-up line unless it would start before
     // the readable bytes (then the 16-B step at or below base - min(halo, 48))
@@ -589,6 +652,10 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
                     : (uint32_t)(16 * (((uint64_t)kLine + delta - hmin) / 16));
   }
   c->last_grid_P = line ? P - delta : P;
+  if (c->stamping && line && c->stamp_meta.size() < c->stamp_cap) {
+    sa.stamp = c->stamp_ring.p + (uint64_t)kStampWords * c->stamp_meta.size();
+    c->stamp_meta.emplace_back(seq, len);
+  }
   if (c->scan_trace && line) {
     c->trace_n = (uint64_t)c->ncu * W;
     const uint64_t slot_words = kScanTraceWords * c->trace_n + 10 * 65536ull;
@@ -664,9 +731,12 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     else                                                                                  \
       hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D, FU>), g, b, 0, ss, sa); \
   } while (0)
+#if DSX_DIAG
     if (line && cc.behind) {
       DSX_LAUNCHL(8, 8, 1, true);
-    } else if (line) {
+    } else
+#endif
+    if (line) {
       DSX_ABLATEL(scanl_kernel, 8, 8, 1)
       DSX_TRACE_VARIANTS(8, 8, 1)
       DSX_LAUNCHL(8, 8, 1, false);
@@ -712,6 +782,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     kp->P = P;
     kp->len = len;
   }
+#if DSX_DIAG
   if (cc.behind) {
     // the call two back finished in this scan, the last one walked in it;
     // this one waits for the next scan (or flush_behind)
@@ -733,6 +804,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     c->stats.pieces++;
     return DSX_OK;
   }
+#endif
   int rc = launch_stitch(c, cc, pc, P, len, is_last, seq, line && c->scan_trace);
   if (rc) return rc;
   if (split) HIPCHK(c, hipEventRecord(c->ev_stitch[par], c->stream));
@@ -898,6 +970,7 @@ int flush_behind(dsx_ctx* c) {
 
 int flush_tasks(dsx_ctx* c) {
   if (c->behind.empty()) return DSX_OK;
+#if DSX_DIAG
   HIPCHK(c, hipSetDevice(c->device));
   // round 1: the walked call's finish and the other's walk (independent);
   // round 2: the latter's finish
@@ -928,12 +1001,16 @@ int flush_tasks(dsx_ctx* c) {
       }
     c->behind.swap(next);
   }
+#endif
   return DSX_OK;
 }
 
 // A queued cut_device call that can be stitched behind later scans: one
 // line-aligned piece from 0, a candidate density the walk tasks' LDS holds.
 static bool behind_ok(dsx_ctx* c, const void* d_blob, uint64_t len, const dsx_params_t* p) {
+#if !DSX_DIAG
+  return false;  // the stitch behind the scan is in libdsx_diag.so only
+#endif
   if (!c->fuse || !c->scan_line || c->stitch_cus > 0 || c->variant) return false;
   if (len == 0 || len > kPieceMax || ((uintptr_t)d_blob & (kLine - 1)) != 0) return false;
   const uint64_t seg = std::max<uint64_t>(c->seg_max_mult * p->max, c->seg_floor);
@@ -1084,7 +1161,10 @@ extern "C" int dsx_cut_device(dsx_ctx_t* c, const void* d_blob, uint64_t len, co
     const bool timed = (flags & DSX_TIMED) != 0;
     c->timing = timed;
     if (timed) std::swap(c->pev, c->q_pev[q.slot]);
-    c->defer_publish = true;
+    // (split streams: the next scan runs on scan_stream and waits only for
+    // the stitch two pieces back, so it could publish a state the previous
+    // stitch is still writing; publish_kernel then runs on the ctx stream)
+    c->defer_publish = c->scan_stream == c->stream;
     rc = run_device(c, (const uint8_t*)d_blob, len, cc);
     c->defer_publish = false;
     if (timed) std::swap(c->pev, c->q_pev[q.slot]);
@@ -1171,6 +1251,7 @@ extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_
 // device).
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream,
                   uint32_t* queue) {
+  const bool own = stream == nullptr;  // the ctx stream: launches run one after another
   if (!stream) stream = c->stream;
   if (!queue) {
     HIPCHK(c, c->dg_queue.ensure(1));
@@ -1209,6 +1290,21 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
   HIPCHK(c, hipMemsetAsync(queue, 0, 4, stream));
   da.queue = queue;
   da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * kDigestThreads);
+  // more chunks than lanes: the queue hands them out longest first (a
+  // counting sort by size class, three small passes on the same stream)
+  if (own && c->digest_lpt && max_n > blocks * kDigestThreads && max_n < (1ull << 32)) {
+    HIPCHK(c, grow(c, c->dg_order, max_n));
+    HIPCHK(c, c->dg_cls.ensure(2 * kSizeClasses));
+    HIPCHK(c, hipMemsetAsync(c->dg_cls.p, 0, kSizeClasses * sizeof(uint32_t), stream));
+    const dim3 tiles((uint32_t)((max_n + kOrderTile - 1) / kOrderTile));
+    hipLaunchKernelGGL(digest_order_count_kernel, tiles, dim3(256), 0, stream, da, c->dg_cls.p);
+    hipLaunchKernelGGL(digest_order_scan_kernel, dim3(1), dim3(kSizeClasses), 0, stream,
+                       (const uint32_t*)c->dg_cls.p, c->dg_cls.p + kSizeClasses);
+    hipLaunchKernelGGL(digest_order_scatter_kernel, tiles, dim3(256), 0, stream, da,
+                       c->dg_cls.p + kSizeClasses, c->dg_order.p);
+    HIPCHK(c, hipGetLastError());
+    da.order = c->dg_order.p;
+  }
   if (algo == DSX_DIGEST_SHA512_256)
     hipLaunchKernelGGL(digest_kernel<Sha512>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
                        stream, da);

@@ -86,7 +86,14 @@ struct ScanArgs {
   const DevState* pub_state;
   HostState* pub_host;
   uint64_t pub_seq;
+  // measurement (dsx_stamps_begin): this launch's stamp record, or null.
+  // Every live wave adds its start/end (s_memrealtime, 100 MHz) and shader
+  // cycles (s_memtime) once, at its first and last instruction.
+  uint64_t* stamp;
 };
+
+// dsx_scan_stamp_t words the scan accumulates into (the host fills seq/bytes)
+constexpr int kStampWords = 8;  // t_first, t_last, wave_cycles, wave_ticks, waves, -, -, -
 
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches
 // of one 128-B line per lane, so the ring phase repeats), offsets in u16

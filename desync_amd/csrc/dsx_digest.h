@@ -25,7 +25,18 @@ struct DigestArgs {
   // Records are {total cuts, carried cut} snapshots of the chain state.
   const uint64_t* range_lo;
   const uint64_t* range_hi;
+  // longest-first queue order (digest_order_*_kernel): queue position k takes
+  // chunk order[k]; null: index order
+  const uint32_t* order;
 };
+
+// Longest-first order of a digest range (LPT): a counting sort of the chunks
+// by size class (8 per octave), largest class first.
+constexpr int kSizeClasses = 512;
+constexpr int kOrderTile = 2048;  // chunks per workgroup of the count / scatter passes
+__global__ void digest_order_count_kernel(DigestArgs a, uint32_t* cls_count);
+__global__ void digest_order_scan_kernel(const uint32_t* cls_count, uint32_t* cls_off);
+__global__ void digest_order_scatter_kernel(DigestArgs a, uint32_t* cls_off, uint32_t* order);
 
 // copies {DevState.total, DevState.carry} into rec[0..1] (the digest range
 // snapshot after a window's stitch)

@@ -449,6 +449,102 @@ __global__ void batch_begin_kernel(DevState* st, uint64_t* rec, int fresh, uint6
   }
 }
 
+// ---- longest-first queue order ---------------------------------------------
+// Chunk sizes vary 16x (min..max).  Handed out in index order, the last chunk
+// a lane draws may be a long one that its wave then compresses nearly alone
+// (a 256 KiB chunk is 2,049 SHA-512 blocks against 513 for the average
+// 64 KiB).  Handed out longest first, the long chains start in the first
+// round and the short ones fill in behind them (LPT scheduling).  Within a
+// size class the order is arbitrary; the IDs land at their chunk index.
+
+// monotone in sz: sz < 8 -> sz, else 8 + 8*(log2(sz) - 3) + the next 3 bits
+__device__ __forceinline__ uint32_t size_class(uint64_t sz) {
+  if (sz < 8) return (uint32_t)sz;
+  const uint32_t lg = 63u - (uint32_t)__builtin_clzll(sz);
+  return 8u + 8u * (lg - 3u) + (uint32_t)((sz >> (lg - 3u)) & 7u);
+}
+
+// the digest range as digest_kernel resolves it
+struct DigestRange {
+  uint64_t n, first_start;
+  const uint64_t* ends;
+};
+__device__ __forceinline__ DigestRange digest_range(const DigestArgs& a) {
+  DigestRange r{a.n, a.first_start, a.ends};
+  if (a.range_lo) {
+    const uint64_t i0 = a.range_lo[0], i1 = a.range_hi[0];
+    r.n = i1 > i0 ? i1 - i0 : 0;
+    r.first_start = a.range_lo[1];
+    r.ends += i0;
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint32_t chunk_class(const DigestRange& r, uint64_t i) {
+  const uint64_t s = i == 0 ? r.first_start : r.ends[i - 1], e = r.ends[i];
+  return size_class(e > s ? e - s : 0);
+}
+
+// pass 1: chunks per size class (block tile of kOrderTile chunks)
+__global__ __launch_bounds__(256) void digest_order_count_kernel(DigestArgs a, uint32_t* cls_count) {
+  __shared__ uint32_t h[kSizeClasses];
+  for (int c = threadIdx.x; c < kSizeClasses; c += blockDim.x) h[c] = 0;
+  __syncthreads();
+  const DigestRange r = digest_range(a);
+  const uint64_t t0 = (uint64_t)blockIdx.x * kOrderTile;
+  for (uint64_t i = t0 + threadIdx.x; i < r.n && i < t0 + kOrderTile; i += blockDim.x)
+    atomicAdd(&h[chunk_class(r, i)], 1u);
+  __syncthreads();
+  for (int c = threadIdx.x; c < kSizeClasses; c += blockDim.x)
+    if (h[c]) atomicAdd(&cls_count[c], h[c]);
+}
+
+// pass 2 (one block of kSizeClasses threads): cls_off[c] = chunks in classes
+// above c (largest class first)
+__global__ __launch_bounds__(kSizeClasses) void digest_order_scan_kernel(const uint32_t* cls_count,
+                                                                         uint32_t* cls_off) {
+  __shared__ uint32_t v[kSizeClasses];
+  const int t = threadIdx.x;              // position in descending class order
+  const int c = kSizeClasses - 1 - t;     // its class
+  v[t] = cls_count[c];
+  __syncthreads();
+  for (int d = 1; d < kSizeClasses; d <<= 1) {  // inclusive scan (Hillis-Steele)
+    const uint32_t x = t >= d ? v[t - d] : 0u;
+    __syncthreads();
+    v[t] += x;
+    __syncthreads();
+  }
+  cls_off[c] = v[t] - cls_count[c];
+}
+
+// pass 3: each block reserves its tile's slots per class, then places its
+// chunks (order within a class: arbitrary)
+__global__ __launch_bounds__(256) void digest_order_scatter_kernel(DigestArgs a, uint32_t* cls_off,
+                                                                   uint32_t* order) {
+  constexpr int PER = kOrderTile / 256;
+  __shared__ uint32_t h[kSizeClasses], base[kSizeClasses];
+  for (int c = threadIdx.x; c < kSizeClasses; c += blockDim.x) h[c] = 0;
+  __syncthreads();
+  const DigestRange r = digest_range(a);
+  const uint64_t t0 = (uint64_t)blockIdx.x * kOrderTile;
+  uint32_t cls[PER], rank[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint64_t i = t0 + (uint64_t)q * 256u + threadIdx.x;
+    cls[q] = i < r.n ? chunk_class(r, i) : 0u;
+    rank[q] = i < r.n ? atomicAdd(&h[cls[q]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < kSizeClasses; c += blockDim.x)
+    base[c] = h[c] ? atomicAdd(&cls_off[c], h[c]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint64_t i = t0 + (uint64_t)q * 256u + threadIdx.x;
+    if (i < r.n) order[base[cls[q]] + rank[q]] = (uint32_t)i;
+  }
+}
+
 template <class H>
 __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
   constexpr int BLK = H::BLK;
@@ -467,15 +563,19 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
     const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
     nfirst = (uint32_t)(n < lanes ? n : lanes);
   }
-  // chunk state (s, e, pos relative to blob[0])
-  uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // first chunk: static
+  // chunk state (s, e, pos relative to blob[0]); k = queue position (the
+  // first one static), ci = its chunk (a.order: longest first)
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t ci = n;
   uint64_t s = 0, e = 0, pos = 0;
   uint32_t phase = 0;  // 0 = data blocks, 1 = tail with marker, 2 = length-only block
   uint32_t raw[BLK / 4 + 4];  // prefetched window of the next full block
   bool have_next = false;
   H st;
   auto start_chunk = [&]() {
-    while (ci < n) {
+    ci = n;
+    while (k < n) {
+      ci = a.order ? (uint64_t)a.order[k] : k;
       const uint64_t sa = ci == 0 ? first_start : ends[ci - 1], ea = ends[ci];
       // a chunk outside the readable bytes (malformed ends) is skipped and
       // gets no ID instead of reading out of bounds
@@ -488,13 +588,14 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
         st.init();
         return;
       }
-      ci = n;  // (this lane takes no further chunk)
+      k = n;  // (this lane takes no further chunk)
+      ci = n;
     }
   };
-  if (ci >= nfirst) ci = n;  // (grid larger than the static share)
+  if (k >= nfirst) k = n;  // (grid larger than the static share)
   start_chunk();
   while (true) {
-    const bool live = ci < n;
+    const bool live = k < n;
     if (__ballot(live) == 0) break;
     uint32_t d[32];
     bool finished = false;
@@ -542,7 +643,7 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
       base = __shfl(base, __ffsll((long long)fm) - 1, 64);
       if (finished) {
         const uint32_t rank = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-        ci = (uint64_t)nfirst + base + rank;
+        k = (uint64_t)nfirst + base + rank;
         start_chunk();
       }
     }

@@ -151,6 +151,9 @@ struct dsx_ctx {
   DevBuf<uint64_t> dg_ends;   // chunk IDs: staged chunk ends
   DevBuf<uint8_t> dg_ids;     // chunk IDs: staged digests
   DevBuf<uint32_t> dg_queue;  // chunk IDs: lane work queue
+  DevBuf<uint32_t> dg_order;  // chunk IDs: longest-first queue order (ctx-stream launches)
+  DevBuf<uint32_t> dg_cls;    // chunk IDs: [kSizeClasses] counts, [kSizeClasses] offsets
+  int digest_lpt = 1;         // DSX_DIGEST_LPT=0: digest_kernel's queue in index order
   DevBuf<DevState> state;
   HostState* h_state = nullptr;  // pinned mirror published by fixup_kernel
   uint64_t piece_seq = 0;        // global piece counter (overflow parity, freshness)
@@ -164,7 +167,7 @@ struct dsx_ctx {
   bool defer_publish = false;       // set while a queued cut_device call is enqueued
   HostState* pub_host = nullptr;    // pending: slot ...
   uint64_t pub_seq = 0;             // ... and piece seq
-  // stitch behind the scan (DSX_FUSE, default on): queued one-piece calls
+  // stitch behind the scan (DSX_FUSE=1, opt-in, off by default): queued one-piece calls
   // whose walk (walked = false) or finish (walked = true) runs as tasks in
   // the next queued call's scan; flush_behind() launches them on their own
   struct Behind {
@@ -175,9 +178,10 @@ struct dsx_ctx {
     uint64_t seq = 0;
   };
   std::deque<Behind> behind;
-  bool fuse = false;  // DSX_FUSE=1 (off: throughput-neutral under the board's power cap)
+  bool fuse = false;  // DSX_FUSE=1, libdsx_diag.so only (throughput-neutral under the board's power cap)
   static constexpr uint32_t kTaskRing = 16;  // > the launches a queued call can be behind
   TaskArgs* h_tasks = nullptr;               // pinned ring: the TaskArgs of fused scans
+  uint64_t fuse_seq = 0;                     // fused calls enqueued (ring index)
   DevBuf<SegInfo> seg_info2;  // the second segment set (calls of odd piece seq)
   DevBuf<uint64_t> stage2;
   DevBuf<uint64_t> spec, spec2;  // stitch tasks' speculative chains (per set)
@@ -249,6 +253,12 @@ struct dsx_ctx {
   uint64_t* h_res = nullptr;  // pinned: shard_emit_kernel status / count / entry
 
   dsx_stats_t stats{};
+  // in-kernel stamps of the scan launches (dsx_stamps_begin .. dsx_stamps_end):
+  // record i (kStampWords words of stamp_ring) belongs to stamp_meta[i] = {seq, bytes}
+  DevBuf<uint64_t> stamp_ring;
+  bool stamping = false;
+  uint64_t stamp_cap = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> stamp_meta;
   // per-piece timing events of the current call: {before scan, after scan, after gather}
   std::vector<hipEvent_t> pev;
   uint32_t npiece_call = 0;
@@ -276,7 +286,7 @@ struct dsx_ctx {
   // windows, chain-state snapshots that delimit each window's digest range
   static constexpr int kIdxSlots = 8;
   uint64_t index_window = 1ull << 30;  // DSX_INDEX_WINDOW: bytes per HBM window
-  uint64_t index_slot = 64ull << 20;   // DSX_INDEX_SLOT: bytes per pinned read slot
+  uint64_t index_slot = 32ull << 20;   // DSX_INDEX_SLOT: bytes per pinned read slot
   int index_readers = 4;               // DSX_INDEX_READERS: reader threads
   uint8_t* idx_slots[kIdxSlots] = {};
   uint64_t idx_slot_bytes = 0;

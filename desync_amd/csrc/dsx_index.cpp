@@ -8,10 +8,10 @@
 // and block devices.
 //
 // Pipeline (one context, two HIP streams, reader threads):
-//   reader threads  pread/memcpy 64 MiB pieces into a ring of pinned slots;
+//   reader threads  pread/memcpy 32 MiB pieces into a ring of pinned slots;
 //   copy_stream     H2D of each piece into the current HBM window;
 //   stream          scan + stitch (dsx_scan.hip, dsx_stitch.hip) every
-//                   256 MiB, the chain state carried on the device; at the
+//                   32 MiB, the chain state carried on the device; at the
 //                   end of a window a snapshot of {total cuts, carried cut}
 //                   and digest_kernel over the chunks the window finished.
 // Two windows alternate, so the digest of window w overlaps the H2D and scan
@@ -139,7 +139,10 @@ int fill_fd(void* ud, uint8_t* dst, uint64_t off, uint64_t n) {
   return DSX_OK;
 }
 
-constexpr uint64_t kScanStep = 256ull << 20;  // bytes per scan + stitch launch
+// bytes per scan + stitch launch: each stitch publishes the chain position
+// (dsx_progress), so 32 per GiB, make.go:138's pb.Set per chunk in steps of
+// 32 MiB; the GPU work per step (~40 us) is far below its PCIe time (~1 ms)
+constexpr uint64_t kScanStep = 32ull << 20;
 
 int index_setup(dsx_ctx* c, uint64_t slot_bytes) {
   if (c->idx_slot_bytes < slot_bytes) {

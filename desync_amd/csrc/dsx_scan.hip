@@ -31,8 +31,12 @@
 #include "../../include/dsx_buzhash_table.h"
 #include <type_traits>
 #include <utility>
+#include "dsx_chain.h"
 #include "dsx_common.h"
+#include "dsx_stitch.h"
+#if DSX_DIAG  // the stitch behind the scan (DSX_FUSE): libdsx_diag.so only
 #include "dsx_tasks.h"
+#endif
 
 namespace dsx {
 
@@ -137,6 +141,33 @@ __device__ __forceinline__ void prefetch4(const u32x4& rsrc, uint32_t voff, uint
       : "=&s"(keep)
       : "v"(voff), "s"(lds_addr), "s"(rsrc)
       : "memory");
+}
+
+// Realtime (100 MHz) and shader-clock counters, read together; the wait sits
+// inside the statement so no counted lgkmcnt of the kernel is disturbed.
+__device__ __forceinline__ void stamp_now(uint64_t& rt, uint64_t& cy) {
+  asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(rt), "=s"(cy)
+               :
+               : "memory");
+}
+
+// One live wave's share of its launch's stamp record (lane 0; vector
+// atomics).  The start half adds -t0 to the span sums and the end half +t1
+// (sums mod 2^64), so nothing stays live across the scan loop.
+__device__ __forceinline__ void stamp_wave(uint64_t* rec, bool end) {
+  uint64_t rt, cy;
+  stamp_now(rt, cy);
+  if ((threadIdx.x & 63) == 0) {
+    if (end) {
+      atomicMax((unsigned long long*)&rec[1], (unsigned long long)rt);
+      atomicAdd((unsigned long long*)&rec[4], 1ull);
+    } else {
+      atomicMin((unsigned long long*)&rec[0], (unsigned long long)rt);
+    }
+    atomicAdd((unsigned long long*)&rec[2], (unsigned long long)(end ? cy : 0ull - cy));
+    atomicAdd((unsigned long long*)&rec[3], (unsigned long long)(end ? rt : 0ull - rt));
+  }
 }
 
 // h % d == d-1 on the GPU.
@@ -649,6 +680,9 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // trace: the wave's first instruction (before the table fill)
   const uint64_t t_entry = VARIANT == 5 ? __builtin_amdgcn_s_memtime()
                                         : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
+  // in-kernel stamps of the launch (dsx_stamps_begin): every wave's first
+  // instruction here, its last one at the end of its regions
+  if (a.stamp) stamp_wave(a.stamp, false);
 
   if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.pub_host)  // the previous piece's state
@@ -803,11 +837,16 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   if (kBal && threadIdx.x < W) s_prog[threadIdx.x] = 0u;
   __syncthreads();
   // (trace: 6 words per wave slot after the scan's records)
-  uint64_t* const task_tr =
+  [[maybe_unused]] uint64_t* const task_tr =
       a.trace ? a.trace + (uint64_t)kScanTraceWords * gridDim.x * W + 6ull * (blockIdx.x * W + wave)
               : nullptr;
   if (!live) {
-    if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
+    if (a.stamp) stamp_wave(a.stamp, true);
+#if DSX_DIAG
+  #if DSX_DIAG
+  if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
+#endif
+#endif
     return;
   }
   // VARIANT 5 (diagnostic, same results): the trace records shader-clock
@@ -1145,6 +1184,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     sh = nsh;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.stamp) stamp_wave(a.stamp, true);
   if (a.trace && lane == 0) {
     uint64_t* tr = a.trace + (uint64_t)kScanTraceWords * (blockIdx.x * W + wave);
     tr[4] = re_cyc;
@@ -1160,17 +1200,20 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
                          : (nreg_done | ((uint64_t)xcc_id << 32) | ((uint64_t)((hw_id >> 8) & 0xFF) << 40));
   }
   // the staging line is free (the last DMA landed at vmcnt(0) above)
+#if DSX_DIAG
   if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
+#endif
 }
 
-#define DSX_SCANL_INST(W, SUB, D)                                                   \
+#define DSX_SCANL_INST(W, SUB, D)                                          \
   template __global__ void scanl_kernel<0, 0, W, SUB, D, false>(ScanArgs); \
   template __global__ void scanl_kernel<1, 0, W, SUB, D, false>(ScanArgs); \
-  template __global__ void scanl_kernel<2, 0, W, SUB, D, false>(ScanArgs); \
-  template __global__ void scanl_kernel<0, 0, W, SUB, D, true>(ScanArgs);  \
-  template __global__ void scanl_kernel<1, 0, W, SUB, D, true>(ScanArgs);  \
-  template __global__ void scanl_kernel<2, 0, W, SUB, D, true>(ScanArgs);
+  template __global__ void scanl_kernel<2, 0, W, SUB, D, false>(ScanArgs);
 #if DSX_DIAG
+// the stitch behind the scan (DSX_FUSE=1): diagnostic build only
+template __global__ void scanl_kernel<0, 0, 8, 8, 1, true>(ScanArgs);
+template __global__ void scanl_kernel<1, 0, 8, 8, 1, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 0, 8, 8, 1, true>(ScanArgs);
 template __global__ void scanl_kernel<2, 1, 8, 8, 1, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 3, 8, 8, 1, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 4, 8, 8, 1, false>(ScanArgs);

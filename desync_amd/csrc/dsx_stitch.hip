@@ -28,7 +28,9 @@
 #include "dsx_chain.h"
 #include "dsx_common.h"
 #include "dsx_stitch.h"
+#if DSX_DIAG  // the stitch behind the scan (DSX_FUSE): libdsx_diag.so only
 #include "dsx_tasks.h"
+#endif
 
 namespace dsx {
 
@@ -872,6 +874,7 @@ template __global__ void finish_kernel<2>(StitchArgs);
 template __global__ void finish_kernel<4>(StitchArgs);
 template __global__ void finish_kernel<8>(StitchArgs);
 
+#if DSX_DIAG
 // The stitch tasks of queued calls that no later scan carried (flush_behind):
 // one task per wave, finish tasks first.
 __global__ __launch_bounds__(256) void stitch_task_kernel(TaskArgs b) {
@@ -882,6 +885,7 @@ __global__ __launch_bounds__(256) void stitch_task_kernel(TaskArgs b) {
   if (t < b.nf) finish_task(b.f, t, b.fseg, b.nf, b.farrive, lane);
   else if (t - b.nf < b.nw) walk_task(b.w, t - b.nf, b.wseg, cand + wave * kTaskCand, lane);
 }
+#endif
 
 // The chain state of a stitch-only pass (a shard re-walked from its true
 // entry over kept candidate lists; normally the scan initialises it).

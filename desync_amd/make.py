@@ -210,7 +210,7 @@ def _run_polled(fn, dctx, progress):
     t.start()
     v, last = ctypes.c_uint64(), 0
     while True:
-        t.join(0.002)
+        t.join(0.0005)
         if lib().dsx_progress(dctx.h, ctypes.byref(v)) == 0 and v.value > last:
             last = v.value
             progress(last)
@@ -346,7 +346,7 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
     are computed.  ``n`` (the reference's worker count) has no effect on the
     result, as in the reference.  ``ctx`` mirrors the Go context: any object
     with a ``done()`` method (or None); when it reports done the call stops
-    between 64 MiB pieces and Interrupted is raised (make.go:201-203).
+    between 32 MiB pieces and Interrupted is raised (make.go:201-203).
     ``pb.Set`` receives the end of the last confirmed chunk while the call
     runs (dsx_progress), from the calling thread.  The reference returns
     ``(index, stats, err)``; here an error is raised and carries the chunks
@@ -403,9 +403,32 @@ class VerifyError(Exception):
     fileseed.go:192)."""
 
 
-def _contiguous_runs(chunks):
-    """Split index chunks into runs whose chunks follow each other (a decoded
-    caibx is one run; a hand-built Index may have gaps or overlaps)."""
+def _chunk_arrays(chunks):
+    """(starts, ends, ids (n, 32) uint8, bad) of an Index's chunks as arrays.
+    A ChunkArray (IndexFromFile's result, a decoded caibx) already holds them:
+    no IndexChunk is built.  ``bad`` marks chunks whose ID is not 32 bytes (a
+    hand-built Index; a ChunkID is [32]byte in the reference, so they can only
+    mismatch)."""
+    if isinstance(chunks, ChunkArray) and chunks._list is None:
+        ends = chunks._ends
+        starts = np.empty_like(ends)
+        if ends.size:
+            starts[0] = 0
+            starts[1:] = ends[:-1]
+        return starts, ends, chunks._ids, None
+    n = len(chunks)
+    starts = np.fromiter((c.Start for c in chunks), dtype=np.uint64, count=n)
+    ends = starts + np.fromiter((c.Size for c in chunks), dtype=np.uint64, count=n)
+    raw = [bytes(c.ID) for c in chunks]
+    bad = np.fromiter((len(r) != 32 for r in raw), dtype=bool, count=n)
+    ids = np.frombuffer(b"".join(r if len(r) == 32 else bytes(32) for r in raw),
+                        dtype=np.uint8).reshape(n, 32)
+    return starts, ends, ids, (bad if bad.any() else None)
+
+
+def _chunk_runs(chunks):
+    """Runs of index chunks that follow each other, as lists of chunks
+    (ChopFile batches each run on its own)."""
     i = 0
     while i < len(chunks):
         j = i + 1
@@ -413,6 +436,14 @@ def _contiguous_runs(chunks):
             j += 1
         yield chunks[i:j]
         i = j
+
+
+def _contiguous_runs(starts, ends):
+    """[lo, hi) index ranges of runs of chunks that follow each other (a
+    decoded caibx is one run; a hand-built Index may have gaps or overlaps)."""
+    cuts = (np.nonzero(starts[1:] != ends[:-1])[0] + 1).tolist()
+    bounds = [0] + cuts + [int(starts.size)]
+    return list(zip(bounds[:-1], bounds[1:]))
 
 
 def VerifyIndex(ctx, name, idx, n=1, pb=None, device=0):
@@ -435,23 +466,24 @@ def VerifyIndex(ctx, name, idx, n=1, pb=None, device=0):
             raise VerifyError(f"index size ({idx.Length()}) does not match file size ({st.st_size})")
         if not idx.Chunks:
             return None
+        starts, ends, want, bad = _chunk_arrays(idx.Chunks)
         with open(name, "rb") as f:
             size = file_size(f.fileno())
             if _stat.S_ISCHR(st.st_mode):  # (no size: read what the index covers)
-                size = max(c.Start + c.Size for c in idx.Chunks)
-            for run in _contiguous_runs(idx.Chunks):
+                size = int(ends.max())
+            for lo, hi in _contiguous_runs(starts, ends):
                 if ctx is not None and getattr(ctx, "done", lambda: False)():
                     break  # the reference stops feeding workers and returns g.Wait()
-                start = run[0].Start
-                ends = np.fromiter((c.Start + c.Size for c in run), dtype=np.uint64, count=len(run))
-                if int(ends.max()) > size:
+                if int(ends[lo:hi].max()) > size:
                     # ReadAt past the end of the file: io.EOF (fileseed.go:187)
                     raise EOFError("EOF")
-                ids = ids_fd(f.fileno(), start, ends, 0, size, device=device)
-                for c, got in zip(run, ids):
-                    if got.tobytes() != bytes(c.ID):
-                        raise VerifyError(f"seed index for {name} doesn't match its data")
-                pb.Add(len(run))
+                got = ids_fd(f.fileno(), int(starts[lo]), ends[lo:hi], 0, size, device=device)
+                differ = (got != want[lo:hi]).any(axis=1)
+                if bad is not None:
+                    differ |= bad[lo:hi]
+                if differ.any():
+                    raise VerifyError(f"seed index for {name} doesn't match its data")
+                pb.Add(hi - lo)
     finally:
         pb.Finish()
     return None

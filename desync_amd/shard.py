@@ -206,7 +206,8 @@ def device_protocol(engine, world):
     mark_error() replaces the record with a DSX_SEAM_ERROR one; gather()
     all-gathers the records; resolve() enqueues the resolve, whose round
     outcome (AGREE_*) lands in a device word; collect() waits and returns
-    ("ok" | "resync" | "peer", agreed) or raises this rank's failure; result().
+    ("ok" | "resync" | "peer", agreed) or raises this rank's failure (leaving the
+    round's agreed code in engine.last_agreed); result().
     With engine.device_agree (RCCL) the ranks agree on the device before the
     wait: fail_code() overwrites the word with AGREE_FAIL and reduce() enqueues
     its MAX all-reduce, so a converged step waits on the host exactly once
@@ -243,7 +244,15 @@ def device_protocol(engine, world):
                 yield
             try:
                 out, agreed = engine.collect()
-            except BaseException as e:  # noqa: BLE001 -- published next round
+            except BaseException as e:  # noqa: BLE001
+                # Agreed FAIL: every peer saw it and is raising PeerFailed in
+                # this round, so this rank's own failure (e.g. its cut list
+                # did not fit) is raised now -- another exchange round would
+                # wait in a collective nobody joins.  Below FAIL (a re-walk
+                # that failed after an OK/RESYNC agreement, the record marked
+                # DSX_SEAM_ERROR): published by one more exchange round.
+                if (getattr(engine, "last_agreed", None) or 0) >= AGREE_FAIL:
+                    raise
                 err = e
                 continue
         else:
@@ -364,8 +373,11 @@ class DeviceShard:
 
     def collect(self):
         d_agreed = ctypes.c_void_p(self.code.data_ptr()) if self.device_agree else None
+        self.agreed.value = 0
         rc = lib().dsx_shard_collect(self.ctx.h, ctypes.c_void_p(self.seam.data_ptr()), d_agreed,
                                      ctypes.byref(self.agreed), ctypes.byref(self.n))
+        # the round's agreed code, also when rc is this rank's own failure
+        self.last_agreed = self.agreed.value if self.device_agree else None
         if rc not in _COLLECT_RC:
             check(rc, self.ctx.h)
         return _COLLECT_RC[rc], (self.agreed.value if self.device_agree else None)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSX_ABI_VERSION 4
+#define DSX_ABI_VERSION 5
 
 /* ---- error codes (negative) ---------------------------------------------- */
 enum {
@@ -97,7 +97,8 @@ int dsx_cancel(dsx_ctx_t *ctx);
  * IndexFromFile (make.go:134-140).  Monotone within a call, the file length
  * once it succeeded.  Like dsx_cancel, safe to call from another thread while
  * the call runs (it reads pinned memory the device publishes into after each
- * 256 MiB piece; it never touches the context's streams). */
+ * 32 MiB piece's stitch, 32 values per GiB; it never touches the context's
+ * streams). */
 int dsx_progress(dsx_ctx_t *ctx, uint64_t *bytes);
 
 /* ---- one-shot cut lists ------------------------------------------------------ */
@@ -313,6 +314,27 @@ int dsx_selftest_boundary(dsx_ctx_t *ctx, const dsx_params_t *p, int mode, uint6
 int dsx_debug_trace(dsx_ctx_t *ctx, uint64_t *out, uint64_t cap, uint64_t *n_scan,
                     uint64_t *n_walk);
 
+/* ---- measurement: in-kernel stamps of the scan launches ----------------------
+ * (bench.py's roofline; replaces no reference interface.)  Between
+ * dsx_stamps_begin and dsx_stamps_end the next max_launches line-scan launches
+ * of ctx record, from inside the kernel, the s_memrealtime ticks (100 MHz) of
+ * their first wave's first instruction and last wave's last instruction, and
+ * the shader-clock cycles (s_memtime) and realtime ticks each wave spent, summed
+ * over the waves: duration = (t_last - t_first) / 100 MHz, mean shader clock =
+ * wave_cycles / wave_ticks * 100 MHz.  No event or extra kernel runs between
+ * the stamped launches.  begin waits for the ctx's queued work; end waits for
+ * the stamped launches and copies min(cap, *n) records in launch order. */
+typedef struct dsx_scan_stamp {
+    uint64_t seq;          /* piece sequence number of the launch */
+    uint64_t bytes;        /* bytes the launch scanned (one piece: <= 8 GiB) */
+    uint64_t t_first, t_last;
+    uint64_t wave_cycles, wave_ticks;
+    uint64_t waves;        /* waves that hashed at least one region */
+    uint64_t reserved;
+} dsx_scan_stamp_t;
+int dsx_stamps_begin(dsx_ctx_t *ctx, uint64_t max_launches);
+int dsx_stamps_end(dsx_ctx_t *ctx, dsx_scan_stamp_t *out, uint64_t cap, uint64_t *n);
+
 /* ---- synthetic inputs (bench / tests; generated on device) ------------------ */
 /* bytes [offset, offset+len) of the seeded uniform stream (splitmix64 of the
  * 8-byte word index), written to d_dst. */
@@ -346,7 +368,7 @@ int dsx_chunk_ids(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, uint64_t sta
  * out_ends: chunk END offsets relative to off (cap entries); ids: 32 bytes per
  * chunk (cap * 32 bytes); both host memory.  DSX_E_CAPACITY sets *n_out to the
  * required count (len/min + 2 always suffices).  Synchronous; dsx_cancel()
- * interrupts it between 64 MiB pieces (DSX_E_INTERRUPTED).
+ * interrupts it between 32 MiB pieces (DSX_E_INTERRUPTED).
  * Partial results (IndexFromFile returns the chunks assembled so far with
  * chunkErr or Interrupted{}, make.go:133-162, :201-203): on DSX_E_INTERRUPTED
  * and DSX_E_IO, out_ends / ids hold the confirmed prefix of the chain (every

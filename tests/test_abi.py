@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.lib().dsx_abi_version() == 4
+    assert _lib.lib().dsx_abi_version() == 5
 
 
 @pytest.mark.parametrize("args,code,msg", [

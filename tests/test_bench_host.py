@@ -26,13 +26,36 @@ def test_cpu_share_reads_omp_num_threads(monkeypatch):
 def test_data_labels_name_the_generator_seeds(monkeypatch):
     monkeypatch.setattr("sys.argv", ["bench.py"])
     a = bench.parse()
-    assert "seed 1" in bench.DATA_LABEL["uniform"].format(seed=a.seed)
+    # the default per-GPU shape is BASELINE config 5's shard at every N
+    assert (a.gib, a.seed, a.workload, a.config) == (32.0, 3, "uniform", "config 5 shard")
+    assert (a.steps, a.warmup) == (20, 5)
+    assert "seed 3" in bench.DATA_LABEL["uniform"].format(seed=a.seed)
     monkeypatch.setattr("sys.argv", ["bench.py", "--workload", "dedup"])
     a = bench.parse()
     assert "seed 2" in bench.DATA_LABEL["dedup"].format(seed=a.seed)
+    assert (a.gib, a.config) == (16.0, "config 3")
+    monkeypatch.setattr("sys.argv", ["bench.py", "--workload", "zeros"])
+    assert bench.parse().config == "config 4"
     monkeypatch.setattr("sys.argv", ["bench.py", "--config5"])
     a = bench.parse()
     assert (a.gib, a.seed, a.workload) == (32.0, 3, "uniform")  # BASELINE config 5's shards
+    monkeypatch.setattr("sys.argv", ["bench.py", "--config2"])
+    a = bench.parse()
+    assert (a.gib, a.seed, a.workload, a.config) == (1.0, 1, "uniform", "config 2")
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gib", "0.25"])
+    a = bench.parse()
+    assert (a.gib, a.seed, a.config) == (0.25, 3, None)
+
+
+def test_traffic_lookup_by_launch_size(tmp_path, monkeypatch):
+    """roofline.traffic is the PMC figure of launches of the same size only."""
+    import json
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "traffic_uniform_64.json").write_text(
+        json.dumps({"bytes": 64, "hbm_bytes_per_launch": 65.0}))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    assert bench.load_traffic("uniform", 64) == 65.0
+    assert bench.load_traffic("uniform", 128) is None
 
 
 def test_cpu_leg_matches_the_sequential_chain():

@@ -1,6 +1,12 @@
 """Stitch behind the scan: queued (DSX_NO_SYNC) dsx_cut_device calls whose
 walk and finish run as tasks inside the next calls' scans.
 
+The fused stitch (DSX_FUSE=1) is in the diagnostic build only (it does not
+move the bench line under the board's power cap), so
+its scenarios run in one child process on libdsx_diag.so
+(test_fused_stitch_diag); the same scenarios without it run here on the
+product library.
+
 Every call's cut list must equal the oracle's chain (chunker.go:206-277)
 whatever runs between the calls: more fused calls, calls that cannot be
 fused (a pointer off the 128-B grid, a dense-candidate parameter set), a
@@ -8,6 +14,9 @@ dsx_sync, a synchronous call, collection at every queue depth.  Suspect
 segments (seams inside zero runs with short segments) take the redo path.
 """
 import ctypes
+import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -57,14 +66,9 @@ class Queue:
         assert np.array_equal(got, ref)
 
 
-@pytest.fixture
-def fctx(monkeypatch):
-    """A context with the stitch behind the scan switched on (DSX_FUSE=1)."""
-    from desync_amd import _lib
-    monkeypatch.setenv("DSX_FUSE", "1")
-    ctx = _lib.Context(0)
-    yield ctx
-    ctx.close()
+def _fused():
+    """The child process runs on libdsx_diag.so with DSX_FUSE=1."""
+    return os.environ.get("DSX_FUSE", "0") == "1"
 
 
 def _blobs():
@@ -87,7 +91,7 @@ def _blobs():
     }
 
 
-def test_behind_sequence(fctx):
+def scenario_sequence(fctx):
     """A run of queued calls, fused and not, collected at depths 1..8."""
     from desync_amd import _lib
     b = _blobs()
@@ -116,8 +120,7 @@ def test_behind_sequence(fctx):
             q.collect()
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_behind_interleaved_sync_calls(monkeypatch, fuse):
+def scenario_interleaved_sync_calls(fctx):
     """A synchronous call, a chunk-ID call and a host-memory call between
     queued ones run after the stitches still behind (DSX_FUSE=1) and after
     the queued calls' pending publish (the next scan publishes a queued call's
@@ -125,8 +128,6 @@ def test_behind_interleaved_sync_calls(monkeypatch, fuse):
     call (its own events) mixes in."""
     import desync_amd
     from desync_amd import _lib
-    monkeypatch.setenv("DSX_FUSE", fuse)
-    fctx = _lib.Context(0)
     b = _blobs()
     q = Queue(fctx)
     q.submit(b["u40"])
@@ -146,17 +147,16 @@ def test_behind_interleaved_sync_calls(monkeypatch, fuse):
         q.collect()
     q.submit(b["u1"])  # the last queued call: collected with no scan after it
     q.collect()
-    fctx.close()
 
 
-def test_behind_redo_on_suspect_segments(monkeypatch):
+def scenario_redo_on_suspect_segments():
     """Short segments (64 KiB floor, 4 x max) with the true chain inside zero
     runs off the segment grid: seams that do not converge.  The tasks publish
     kErrRedo and dsx_result redoes the call with fixup_kernel's repair."""
     from desync_amd import _lib
-    monkeypatch.setenv("DSX_SEG_FLOOR", "65536")
-    monkeypatch.setenv("DSX_FUSE", "1")
+    os.environ["DSX_SEG_FLOOR"] = "65536"
     ctx = _lib.Context(0)
+    del os.environ["DSX_SEG_FLOOR"]
     try:
         rng = np.random.default_rng(11)
         null = np.zeros(4 * MAX, np.uint8)
@@ -175,7 +175,7 @@ def test_behind_redo_on_suspect_segments(monkeypatch):
         ctx.close()
 
 
-def test_behind_timed_calls(fctx):
+def scenario_timed_calls(fctx):
     """DSX_TIMED fused calls report the scan kernel's time (it carries the
     stitch tasks of the calls behind it) and no separate stitch time."""
     from desync_amd import _lib
@@ -189,41 +189,104 @@ def test_behind_timed_calls(fctx):
         assert 0 < st.scan_ms < 100 and st.stitch_ms == 0
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_bench_steady_state_counts(monkeypatch, fuse):
-    """bench.py's shape: 1 GiB uniform jobs queued 4 deep on one context give
-    the same cut list as the oracle, with and without the fused stitch."""
+def scenario_bench_steady_state_counts(ctx):
+    """bench.py's config-2 shape: 1 GiB uniform jobs queued 4 deep on one
+    context give the same cut list as the oracle."""
     import torch
     from desync_amd import _lib
-    monkeypatch.setenv("DSX_FUSE", fuse)
-    ctx = _lib.Context(0)
-    try:
-        n = 1 << 30
-        arr = o.synth_uniform(1, 0, n)
-        ref = o.chunk_parallel(arr, MIN, AVG, MAX, 16)
-        t = torch.from_numpy(arr).to("cuda")
-        del arr
-        import desync_amd
-        p = desync_amd.Params(MIN, AVG, MAX)
-        L = _lib.lib()
-        outs = [torch.empty(n // MIN + 4, dtype=torch.int64, device="cuda") for _ in range(4)]
-        cnt = ctypes.c_uint64()
-        pend = []
-        for s in range(12):
-            if len(pend) == 4:
-                i = pend.pop(0)
-                _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
-                assert cnt.value == ref.size
-                assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
-            _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(t.data_ptr()), n, ctypes.byref(p.c),
-                                        ctypes.c_void_p(outs[s % 4].data_ptr()), n // MIN + 4,
-                                        ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
-                       ctx.h)
-            pend.append(s % 4)
-        while pend:
+    n = 1 << 30
+    arr = o.synth_uniform(1, 0, n)
+    ref = o.chunk_parallel(arr, MIN, AVG, MAX, 16)
+    t = torch.from_numpy(arr).to("cuda")
+    del arr
+    import desync_amd
+    p = desync_amd.Params(MIN, AVG, MAX)
+    L = _lib.lib()
+    outs = [torch.empty(n // MIN + 4, dtype=torch.int64, device="cuda") for _ in range(4)]
+    cnt = ctypes.c_uint64()
+    pend = []
+    for s in range(12):
+        if len(pend) == 4:
             i = pend.pop(0)
             _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
             assert cnt.value == ref.size
             assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
+        _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(t.data_ptr()), n, ctypes.byref(p.c),
+                                    ctypes.c_void_p(outs[s % 4].data_ptr()), n // MIN + 4,
+                                    ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
+                   ctx.h)
+        pend.append(s % 4)
+    while pend:
+        i = pend.pop(0)
+        _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
+        assert cnt.value == ref.size
+        assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
+
+
+# ---- product library (no fused stitch) ----------------------------------------
+def _ctx():
+    from desync_amd import _lib
+    return _lib.Context(0)
+
+
+def test_interleaved_sync_calls():
+    ctx = _ctx()
+    try:
+        scenario_interleaved_sync_calls(ctx)
     finally:
         ctx.close()
+
+
+def test_bench_steady_state_counts():
+    ctx = _ctx()
+    try:
+        scenario_bench_steady_state_counts(ctx)
+    finally:
+        ctx.close()
+
+
+def test_fuse_needs_the_diagnostic_build(monkeypatch):
+    """DSX_FUSE=1 against the product library is refused loudly (a fresh
+    interpreter: the library is loaded once per process)."""
+    env = dict(os.environ, DSX_FUSE="1")
+    env.pop("DSX_LIB_PATH", None)
+    r = subprocess.run([sys.executable, "-c", "from desync_amd import _lib; _lib.lib()"],
+                       env=env, capture_output=True, text=True, timeout=120, cwd=REPO)
+    assert r.returncode != 0 and "libdsx_diag" in r.stderr
+
+
+# ---- the fused stitch: libdsx_diag.so, one child process ----------------------
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIAG = os.path.join(REPO, "desync_amd", "libdsx_diag.so")
+
+
+@pytest.mark.skipif(not os.path.exists(DIAG), reason="libdsx_diag.so not built (make -C desync_amd/csrc diag)")
+def test_fused_stitch_diag():
+    env = dict(os.environ, DSX_LIB_PATH=DIAG, DSX_FUSE="1", PYTHONPATH=REPO)
+    r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__)], env=env,
+                       capture_output=True, text=True, timeout=900, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "fused stitch scenarios ok" in r.stdout
+
+
+def _main():
+    assert _fused() and os.path.basename(os.environ["DSX_LIB_PATH"]).startswith("libdsx_diag")
+    from desync_amd import _lib
+    for name, f in (("sequence", scenario_sequence),
+                    ("interleaved", scenario_interleaved_sync_calls),
+                    ("timed", scenario_timed_calls),
+                    ("bench", scenario_bench_steady_state_counts)):
+        ctx = _lib.Context(0)
+        try:
+            f(ctx)
+        finally:
+            ctx.close()
+        print("ok:", name, flush=True)
+    scenario_redo_on_suspect_segments()
+    print("ok: redo", flush=True)
+    print("fused stitch scenarios ok", flush=True)
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, REPO)
+    _main()

@@ -234,6 +234,29 @@ def test_index_progress(tmp_path, monkeypatch):
     assert all(v in ends for v in sets), [v for v in sets if v not in ends][:5]
 
 
+def test_index_progress_granularity(tmp_path):
+    """Default pipeline geometry over 1 GiB: the progress bar sees the chain
+    advance in steps of the 32 MiB scan pieces -- at least 16 distinct
+    confirmed-chunk ends per GiB (make.go:138 sets it per chunk)."""
+    import desync_amd
+    data = o.synth_uniform(45, 0, 1 << 30)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    pb = _RecordingBar()
+    desync_amd._lib.reset_context_pool()
+    try:
+        index, _ = desync_amd.IndexFromFile(None, str(f), 4, MIN, AVG, MAX, pb=pb)
+    finally:
+        desync_amd._lib.reset_context_pool()
+    sets = pb.sets()
+    ref = o.chunk_parallel(data, MIN, AVG, MAX, 8)
+    assert len(index.Chunks) == ref.size
+    assert sets == sorted(sets) and sets[-1] == data.size
+    assert len(set(sets)) >= 16, len(set(sets))
+    ends = set(ref.tolist())
+    assert all(v in ends for v in sets)
+
+
 def test_index_partial_on_io_error(tmp_path, monkeypatch):
     """A read error mid-file (the range runs past the end of the file): the
     error carries the confirmed prefix -- IndexFromFile returns the chunks

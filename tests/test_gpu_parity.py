@@ -551,6 +551,57 @@ def test_chunk_ids_both_kernels(monkeypatch, pc, algo):
         ctx.close()
 
 
+@pytest.mark.parametrize("lpt", ["1", "0"])
+@pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
+def test_chunk_ids_longest_first(monkeypatch, lpt, algo):
+    """More chunks than digest_kernel has lanes (~200 K, sizes 0 .. 1000 B
+    with a few of 100 KiB and empty ones): the queue hands them out longest
+    first (DSX_DIGEST_LPT=1, the default: a counting sort by size class) or in
+    index order (0); every ID lands at its chunk's index either way."""
+    import hashlib
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_DIGEST_PC", "0")
+    monkeypatch.setenv("DSX_DIGEST_LPT", lpt)
+    ctx = _lib.Context(0)
+    try:
+        rng = np.random.default_rng(13)
+        total = (100 << 20) + 3
+        arr = rng.integers(0, 256, size=total, dtype=np.uint8)
+        t = torch_dev(arr)
+        sizes = rng.integers(0, 1000, size=220_000)
+        sizes[rng.integers(0, sizes.size, 60)] = 100 << 10
+        ends = np.cumsum(sizes).astype(np.uint64)
+        ends = ends[ends <= total]
+        assert ends.size > 150_000
+        code = _lib.DSX_DIGEST_SHA512_256 if algo == "sha512-256" else _lib.DSX_DIGEST_SHA256
+        name = "sha512_256" if algo == "sha512-256" else "sha256"
+        got = desync_amd.chunk_ids(t.data_ptr(), total, ends, 0, ctx=ctx, algo=code)
+        starts = np.concatenate([np.zeros(1, np.uint64), ends[:-1]])
+        buf = arr.tobytes()
+        for i, (s0, e0) in enumerate(zip(starts.tolist(), ends.tolist())):
+            assert got[i] == hashlib.new(name, buf[s0:e0]).digest(), (i, s0, e0)
+    finally:
+        ctx.close()
+
+
+def test_index_host_longest_first_range(dctx):
+    """dsx_index_host with min/avg/max = 64/256/1024 over 48 MiB: ~190 K chunks
+    in one window, so the window's digest takes the longest-first order of a
+    device-side range (the chunk count is read on the device); cuts equal the
+    oracle's chain, IDs hashlib's."""
+    import hashlib
+    import desync_amd
+    arr = o.synth_uniform(17, 0, (48 << 20) + 5)
+    ends, ids = desync_amd.index_host(arr, 64, 256, 1024, ctx=dctx)
+    ref = o.chunk_stream(arr, 64, 256, 1024)
+    assert np.array_equal(ends, ref) and ref.size > 150_000
+    starts = np.concatenate([np.zeros(1, np.uint64), ref[:-1]])
+    buf = arr.tobytes()
+    for i, (s0, e0) in enumerate(zip(starts.tolist(), ref.tolist())):
+        assert bytes(ids[i]) == hashlib.new("sha512_256", buf[s0:e0]).digest(), i
+
+
 def test_chunk_ids_default_chunking(dctx):
     """IDs of the real chunking of a 64 MiB seeded blob (config-2 shape)."""
     import hashlib

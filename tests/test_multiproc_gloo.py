@@ -135,6 +135,9 @@ class OracleDeviceEngine(OracleEngine):
         if self.sh.failed_ranks(self.allb, self.world):
             self.pend, self.code = ("peer",), 2
             return
+        if self.fail == "capacity":  # the device resolve's own FAIL code (cut list too long)
+            self.pend, self.code = ("capacity",), 2
+            return
         seams = [_from_struct(s) for s in self.sh.seams_from_bytes(self.allb, self.world)]
         self.pend = oseam.resolve(seams, self.rank, MIN, MAX)
         self.code = 0 if self.pend[0] == "ok" else 1
@@ -148,6 +151,9 @@ class OracleDeviceEngine(OracleEngine):
     def collect(self):
         from oracle import seam as oseam
         agreed = self.agreed if self.device_agree else None
+        self.last_agreed = agreed
+        if self.pend[0] == "capacity":  # dsx_shard_collect: this rank's own failure
+            raise IOError("injected capacity failure")
         if agreed == 2 or self.pend[0] == "peer":
             return "peer", agreed
         st, a, b = self.pend
@@ -294,12 +300,14 @@ def test_device_protocol_gloo(kind, world, device_agree):
 @pytest.mark.parametrize("device_agree", [True, False])
 @pytest.mark.parametrize("fail,world,fail_rank", [("start", 2, 0), ("start", 3, 2),
                                                   ("resolve", 3, 1), ("rewalk", 2, 1),
-                                                  ("rewalk", 3, 1)])
+                                                  ("rewalk", 3, 1), ("capacity", 2, 1),
+                                                  ("capacity", 3, 0)])
 def test_device_protocol_failure_propagates(fail, world, fail_rank, device_agree):
     """A rank failing before its round code is known (start, resolve) or after
-    the device agreement (its re-walk, on a zero run across every seam): the
-    failing rank raises its own error, every other rank PeerFailed, nobody
-    hangs."""
+    the device agreement (its re-walk, on a zero run across every seam), or
+    its collect raising its own error after the ranks agreed FAIL (a cut list
+    that does not fit: the peers already raise in that round): the failing
+    rank raises its own error, every other rank PeerFailed, nobody hangs."""
     kind = "seam-zero-run" if fail == "rewalk" else "random"
     msgs = _drun(_compose(kind), world, fail_rank, fail, device_agree)
     kinds = sorted((m[1], m[0]) for m in msgs)
