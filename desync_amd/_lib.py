@@ -80,6 +80,7 @@ class Stats(ctypes.Structure):
         ("chunks", ctypes.c_uint64), ("candidates", ctypes.c_uint64), ("pieces", ctypes.c_uint64),
         ("repaired_segments", ctypes.c_uint64), ("dense_fallbacks", ctypes.c_uint64),
         ("scan_ms", ctypes.c_float), ("stitch_ms", ctypes.c_float),
+        ("chunks_discarded", ctypes.c_uint64),
     ]
 
 

@@ -1029,6 +1029,7 @@ static int finish_call(dsx_ctx* c, uint64_t* n_out, uint64_t cap, bool* dense_re
   }
   c->stats.chunks = s.total;
   c->stats.repaired_segments = s.repaired;
+  c->stats.chunks_discarded = s.discarded;
   float scan = 0, stitch = 0;
   for (uint32_t i = 0; i < c->npiece_call; ++i) {
     float a = 0, b = 0;
@@ -1104,6 +1105,7 @@ extern "C" int dsx_result(dsx_ctx_t* c, uint64_t* n_out) {
   }
   c->stats.chunks = s.total;
   c->stats.repaired_segments = s.repaired;
+  c->stats.chunks_discarded = s.discarded;
   float scan = 0, stitch = 0;  // untimed queued calls record no events
   for (uint32_t i = 0; i < q.npiece; ++i) {
     float a = 0, b = 0;

@@ -23,6 +23,7 @@ __device__ __forceinline__ void publish_state(volatile HostState* h, const DevSt
   h->carry = st->carry;
   h->total = st->total;
   h->repaired = st->repaired;
+  h->discarded = st->discarded;
   h->done = st->done;
   h->err = st->err;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

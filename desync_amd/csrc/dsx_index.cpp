@@ -327,6 +327,8 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       return DSX_E_INTERNAL;
     }
     c->stats.chunks = st.total;
+    c->stats.repaired_segments = st.repaired;
+    c->stats.chunks_discarded = st.discarded;
     *n_out = st.total;
     if (st.total > cap) return DSX_E_CAPACITY;
     if (st.total) {

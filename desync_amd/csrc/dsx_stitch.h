@@ -55,11 +55,12 @@ struct DevState {
   uint64_t base;        // total at the start of the piece's stitch
   uint32_t skip;        // done or overflow at that point
   uint32_t pad2;
+  uint64_t discarded;   // staged cuts a repair replaced (ChunksProduced - ChunksAccepted)
 };
 
 // Published by the last kernel of a piece into pinned host memory.
 struct HostState {
-  uint64_t carry, total, repaired;
+  uint64_t carry, total, repaired, discarded;
   uint32_t done, err;
   uint64_t seq;  // piece sequence number, for the host to check freshness
 };

@@ -169,6 +169,7 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
       st->total = 0;
       st->piece_cuts = 0;
       st->repaired = 0;
+      st->discarded = 0;
       st->done = 0;
       st->err = 0;
       st->active = 0;
@@ -440,6 +441,7 @@ __device__ void fixup_body(const StitchArgs& a, bool do_publish = true) {
     GlobalSrc src{&a.pc};
     const uint64_t s0 = st->carry;
     uint32_t fi = 0, repaired = 0;
+    uint64_t discarded = 0;  // staged cuts the repairs replaced
     uint32_t k = a.flag_list[0];
     bool rp = false;  // was segment k-1 repaired?
     uint64_t rex = 0; // its repaired exit
@@ -483,12 +485,14 @@ __device__ void fixup_body(const StitchArgs& a, bool do_publish = true) {
       if (n > a.scap) st->err |= kErrCapacity;
       a.rep_cnt[k] = n;
       if (!joined) a.rep_from[k] = scnt;
+      discarded += a.rep_from[k];
       ++repaired;
       rp = true;
       rex = joined ? si.Z : last;
       ++k;
     }
     st->repaired += repaired;
+    st->discarded += discarded;
   }
   __syncthreads();
 
@@ -895,6 +899,7 @@ __global__ void state_init_kernel(DevState* st, uint64_t carry) {
     st->total = 0;
     st->piece_cuts = 0;
     st->repaired = 0;
+    st->discarded = 0;
     st->done = 0;
     st->err = 0;
     st->active = 0;

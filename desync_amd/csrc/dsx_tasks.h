@@ -317,6 +317,7 @@ __device__ __attribute__((noinline)) void finish_task(const FinishJob& fr, uint3
     h->carry = mk >= 0 ? reinterpret_cast<const TaskSeg*>(f.seg_info)[mk].Z : 0ull;  // the last cut
     h->total = (!ovf && !any_bad) ? total : 0ull;
     h->repaired = 0;
+    h->discarded = 0;
     h->done = 1;
     h->err = (ovf ? kErrDense : 0u) | (!ovf && any_bad ? kErrRedo : 0u) |
              (!ovf && !any_bad && !fits ? kErrCapacity : 0u);

@@ -238,13 +238,14 @@ def _partial_error(rc, dctx, **partial):
 
 
 def index_fd(fd, min_size, avg_size, max_size, offset=0, length=None, algo=None, ctx=None,
-             device=0, cancel=None, progress=None):
+             device=0, cancel=None, progress=None, stats=None):
     """dsx_index_fd: a file range -> (chunk end offsets relative to ``offset``,
     uint8 array of 32-byte chunk IDs), both computed on the GPU.  ``length``
     None means to the end (files and block devices).  ``progress(bytes)`` is
     called with the end of the last confirmed chunk as the call advances.  On
     cancellation (Interrupted) or a read error (DsxError DSX_E_IO) the raised
-    exception carries the confirmed prefix as ``.ends`` / ``.ids``."""
+    exception carries the confirmed prefix as ``.ends`` / ``.ids``.  ``stats``
+    (a dict) receives the call's dsx_stats_t fields."""
     p = Params(min_size, avg_size, max_size)
     code = _digest_code(algo)
     size = length if length is not None else max(0, file_size(fd) - offset)
@@ -261,6 +262,9 @@ def index_fd(fd, min_size, avg_size, max_size, offset=0, length=None, algo=None,
         if rc in (_lib.DSX_E_INTERRUPTED, _lib.DSX_E_IO):
             raise _partial_error(rc, c, ends=ends[:n.value].copy(), ids=ids[:n.value].copy())
         check(rc, c.h)
+        if stats is not None:
+            st = c.stats()
+            stats.update({k: getattr(st, k) for k, _ in st._fields_})
 
     if ctx is not None:
         call(ctx)
@@ -361,10 +365,14 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
     Params(min_size, avg_size, max_size)  # NewChunker validation, make.go:103
     index = Index(FormatIndex(flags, min_size, avg_size, max_size), [])
 
+    call_stats = {}
+
     def assemble(ends, ids):
         index.Chunks = ChunkArray(ends, ids)  # (IndexChunk objects built on access)
         stats.ChunksAccepted = len(index.Chunks)
-        stats.ChunksProduced = len(index.Chunks)
+        # make.go:329-341 also counts the chunks workers produced and syncWith
+        # dropped; here: the staged cuts a stitch repair replaced
+        stats.ChunksProduced = len(index.Chunks) + int(call_stats.get("chunks_discarded", 0))
 
     with open(name, "rb") as f:
         head = f.read(64)
@@ -381,7 +389,8 @@ def IndexFromFile(ctx, name, n, min_size, avg_size, max_size, pb=None, device=0)
                 # pb.Set(chunk.Start + chunk.Size) as chunks are confirmed (make.go:138)
                 ends, ids = index_fd(f.fileno(), min_size, avg_size, max_size, 0, size,
                                      device=device, cancel=ctx,
-                                     progress=None if isinstance(pb, NullProgressBar) else pb.Set)
+                                     progress=None if isinstance(pb, NullProgressBar) else pb.Set,
+                                     stats=call_stats)
             except (Interrupted, _lib.DsxError) as e:
                 # make.go:133-162 returns the chunks assembled so far with the
                 # error: here the raised error carries them (.index, .stats)

@@ -404,6 +404,9 @@ typedef struct dsx_stats {
     uint64_t repaired_segments; /* segments that needed the sequential repair */
     uint64_t dense_fallbacks;   /* pieces processed on the dense-candidate path */
     float scan_ms, stitch_ms;   /* device time of the last synchronous call (HIP events; 0 after dsx_result) */
+    uint64_t chunks_discarded;  /* cuts the stitch computed, then replaced by a repair: ChunksProduced
+                                   = chunks + chunks_discarded (make.go:329-341 counts the workers'
+                                   discarded overlap chunks too) */
 } dsx_stats_t;
 int dsx_get_stats(dsx_ctx_t *ctx, dsx_stats_t *out);
 

@@ -8,7 +8,8 @@
 #   3. config 2's 1 GiB shape under the same protocol, DSX_FUSE 0/1 in
 #      alternating fresh processes (both on libdsx_diag.so, which holds the
 #      fused stitch);
-#   4. per-launch in-kernel stamps from idle and after a 1 s gap.
+#   4. per-launch in-kernel stamps from idle and after a 1 s gap;
+#   5. energy per GiB of the staging alternatives (tools/ubench_energy.hip).
 # Outputs under gpurun_out/$TAG/.
 set -o pipefail
 export TMPDIR=/tmp
@@ -38,4 +39,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_c2 -o run --out
 timeout -k 10 200 python3 tools/cold_regime.py --gib 1 --jobs 60 --out $OUT/cold_1g.json > $OUT/cold_1g.txt 2> $OUT/cold_1g.err || { tail $OUT/cold_1g.err; exit 1; }
 timeout -k 10 200 python3 tools/cold_regime.py --gib 32 --seed 3 --jobs 12 --out $OUT/cold_32g.json > $OUT/cold_32g.txt 2> $OUT/cold_32g.err || { tail $OUT/cold_32g.err; exit 1; }
 head -30 $OUT/cold_1g.txt
+if [ -x tools/ubench_energy ]; then
+  timeout -k 10 180 ./tools/ubench_energy 8 1.5 > $OUT/ubench_energy.txt 2>&1 || { tail $OUT/ubench_energy.txt; exit 1; }
+  cat $OUT/ubench_energy.txt
+fi
 echo done
