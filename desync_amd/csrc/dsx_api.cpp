@@ -514,10 +514,10 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   uint32_t *rcnt, *rlist;
   KeptPiece* kp = nullptr;
   if (cc.keep) {
-    cc.keep->emplace_back();
-    kp = &cc.keep->back();
-    HIPCHK(c, kp->cnt.ensure(nregions));
-    HIPCHK(c, kp->list.ensure(nregions * rcap));
+    if (c->sh.nkept == cc.keep->size()) cc.keep->emplace_back();
+    kp = &(*cc.keep)[c->sh.nkept++];
+    HIPCHK(c, grow(c, kp->cnt, nregions));  // (reused across runs: grows once)
+    HIPCHK(c, grow(c, kp->list, nregions * rcap));
     rcnt = kp->cnt.p;
     rlist = kp->list.p;
   } else {
@@ -1405,6 +1405,7 @@ static void release_kept(dsx_ctx* c) {
     k.list.release();
   }
   c->sh.kept.clear();
+  c->sh.nkept = 0;
 }
 
 // Chunks the shard from the cut `entry` (shard_start: speculative, make.go's
@@ -1428,7 +1429,7 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
   const uint64_t wend0 = sh.start + std::min<uint64_t>(sh.len, 32 * p->max);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, grow(c, c->d_seam, 1));
-  const bool stitch_only = rewalk && !sh.dense && !sh.kept.empty();
+  const bool stitch_only = rewalk && !sh.dense && sh.nkept > 0;
   for (int attempt = 0; attempt < 2; ++attempt) {
     if (c->cancel.load()) return DSX_E_INTERRUPTED;
     HIPCHK(c, grow(c, c->out, need));
@@ -1443,18 +1444,18 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
                          entry);
       HIPCHK(c, hipGetLastError());
       c->npiece_call = 0;
-      for (size_t i = 0; i < sh.kept.size() && !rc; ++i) {
+      for (size_t i = 0; i < sh.nkept && !rc; ++i) {
         PieceCands pc = sh.kept[i].pc;
         pc.overflow = c->zero_word.p;  // (the scan succeeded: no overflow)
         rc = launch_stitch(c, cc, pc, sh.kept[i].P, sh.kept[i].len,
-                           is_last && i + 1 == sh.kept.size(), ++c->piece_seq, false);
+                           is_last && i + 1 == sh.nkept, ++c->piece_seq, false);
       }
       if (rc) return rc;
       hipLaunchKernelGGL(seam_cands_kernel, dim3(1), dim3(64), 0, c->stream, sh.kept[0].pc,
                          sh.start, wend0, c->d_seam.p);
       HIPCHK(c, hipGetLastError());
     } else {
-      release_kept(c);
+      sh.nkept = 0;  // (the buffers are reused)
       cc.keep = dense ? nullptr : &sh.kept;
       sh.dense = dense;
       rc = reset_state(c, entry);

@@ -245,7 +245,11 @@ struct dsx_ctx {
     uint64_t pend_cap = 0;
     bool valid = false;
     bool dense = false;                // scanned on the dense path (lists not kept)
-    std::vector<KeptPiece> kept;       // the shard's pieces' region lists
+    // the shard's pieces' region lists: kept[0 .. nkept) of this run; the
+    // buffers stay allocated across runs (a hipFree per step would wait for
+    // the whole device, serialising the bench's pipeline lanes)
+    std::vector<KeptPiece> kept;
+    size_t nkept = 0;
   } sh;
   DevBuf<dsx_seam_t> d_seam, d_all;
   DevBuf<uint32_t> zero_word;  // an overflow flag that stays 0 (stitch-only re-runs)
@@ -334,7 +338,7 @@ struct CallCfg {
   uint64_t out_cap;
   bool dense;        // dense-candidate path
   uint64_t halo0 = 0;  // readable bytes before the first piece (shards)
-  std::vector<KeptPiece>* keep = nullptr;  // keep every piece's region lists here
+  std::vector<KeptPiece>* keep = nullptr;  // keep every piece's region lists here (sh.nkept counts them)
   bool behind = false;  // one queued piece from 0: stitch behind later scans
 };
 
