@@ -315,10 +315,19 @@ def test_stitch_many_workgroups_and_repairs(monkeypatch):
             d = np.concatenate(parts)
             assert np.array_equal(gpu_cut(ctx, d), o.chunk_stream(d, MIN, AVG, MAX))
             if parts[0] is not null:
-                st = ctx.stats()
-                # the repair replaced staged cuts: ChunksProduced > ChunksAccepted
-                assert st.repaired_segments > 0 and st.chunks_discarded > 0
+                assert ctx.stats().repaired_segments > 0
             assert np.array_equal(gpu_cut(ctx, d, mn, av, mx), o.chunk_stream(d, mn, av, mx))
+        # a true chain off the max lattice through 6 segments of zeros (the
+        # last cut of a random megabyte before them): every zero segment's
+        # staged chain, entered from the speculative exit, misses the true
+        # one, so the repair replaces its staged cuts -- the chunks make.go
+        # would count as produced and dropped (ChunksProduced > ChunksAccepted)
+        d = np.concatenate([rng.integers(0, 256, 1 << 20, dtype=np.uint8),
+                            np.zeros(6 << 20, np.uint8), r1])
+        assert np.array_equal(gpu_cut(ctx, d), o.chunk_stream(d, MIN, AVG, MAX))
+        st = ctx.stats()
+        assert st.repaired_segments > 0 and st.chunks_discarded > 0, (st.repaired_segments,
+                                                                       st.chunks_discarded)
     finally:
         ctx.close()
 

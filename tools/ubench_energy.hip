@@ -14,7 +14,8 @@
 //   C reg_lane    each lane loads its own line, 8 x global_load_dwordx4 nt
 //                 straight to VGPRs, the next line in flight (no LDS);
 //   D coalesced   a plain coalesced stream (each wave instruction 1 KiB
-//                 contiguous), the HBM read floor.
+//                 contiguous), the HBM read floor;
+//   A with the other cache policies of the line loads (none, sc1, sc0 sc1 nt).
 //   hipcc --offload-arch=gfx950 -O3 tools/ubench_energy.hip -o tools/ubench_energy
 //   ./tools/ubench_energy [GiB=8] [seconds=1.5]
 #include <hip/hip_runtime.h>
@@ -42,26 +43,34 @@
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kS = 8448;  // lane segment (scanl's default at 1 GiB)
 
-// 8 LDS-DMA wave instructions, 1 KiB each, M0 stepped by 1 KiB (scanl's DMA8, nt)
+// 8 LDS-DMA wave instructions, 1 KiB each, M0 stepped by 1 KiB (scanl's DMA8);
+// POL: 1 nt (scanl's default), 0 none, 2 sc1, 3 sc0 sc1 nt
+#define DMA8(POLSTR)                                                                        \
+  asm volatile(                                                                             \
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %9\n\ts_nop 0\n\t"                                  \
+      "buffer_load_dwordx4 %1, %10, 0 offen " POLSTR "lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t" \
+      "buffer_load_dwordx4 %2, %10, 0 offen " POLSTR "lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t" \
+      "buffer_load_dwordx4 %3, %10, 0 offen " POLSTR "lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t" \
+      "buffer_load_dwordx4 %4, %10, 0 offen " POLSTR "lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t" \
+      "buffer_load_dwordx4 %5, %10, 0 offen " POLSTR "lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t" \
+      "buffer_load_dwordx4 %6, %10, 0 offen " POLSTR "lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t" \
+      "buffer_load_dwordx4 %7, %10, 0 offen " POLSTR "lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t" \
+      "buffer_load_dwordx4 %8, %10, 0 offen " POLSTR "lds\n\ts_mov_b32 m0, %0"               \
+      : "=&s"(keep)                                                                         \
+      : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), "v"(vo[6]),  \
+        "v"(vo[7]), "s"(lds), "s"(rsrc)                                                     \
+      : "memory", "scc")
+template <int POL>
 __device__ __forceinline__ void dma8(const u32x4& rsrc, const uint32_t (&vo)[8], uint32_t lds) {
   uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %9\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %10, 0 offen nt lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %10, 0 offen nt lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %3, %10, 0 offen nt lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %4, %10, 0 offen nt lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %5, %10, 0 offen nt lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %6, %10, 0 offen nt lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %7, %10, 0 offen nt lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %8, %10, 0 offen nt lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), "v"(vo[6]),
-        "v"(vo[7]), "s"(lds), "s"(rsrc)
-      : "memory", "scc");
+  if constexpr (POL == 1) DMA8("nt ");
+  else if constexpr (POL == 2) DMA8("sc1 ");
+  else if constexpr (POL == 3) DMA8("sc0 sc1 nt ");
+  else DMA8("");
 }
+#undef DMA8
 
-template <bool COPY>
+template <bool COPY, int POL>
 __global__ __launch_bounds__(512, 1) void k_dma(const uint8_t* base, uint32_t nregions, uint32_t* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[8 * 8192];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -85,7 +94,7 @@ __global__ __launch_bounds__(512, 1) void k_dma(const uint8_t* base, uint32_t nr
     uint32_t vo[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) vo[i] = dbase[i];
-    dma8(rs, vo, stage);
+    dma8<POL>(rs, vo, stage);
     for (uint32_t b = 0; b < kS / 128; ++b) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (COPY) {
@@ -100,7 +109,7 @@ __global__ __launch_bounds__(512, 1) void k_dma(const uint8_t* base, uint32_t nr
       if (b + 1 < kS / 128) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) vo[i] = dbase[i] + (b + 1) * 128u;
-        dma8(rs, vo, stage);
+        dma8<POL>(rs, vo, stage);
       }
     }
   }
@@ -222,7 +231,7 @@ int main(int argc, char** argv) {
   const double idle = smp.stop();
   printf("buffer %.2f GiB, lane segment %u B, hwmon files %zu, idle %.1f W\n", len / 1073741824.0, kS,
          smp.files.size(), idle);
-  printf("%-12s %9s %9s %8s %8s %9s\n", "variant", "ms/GiB", "TB/s", "W(med)", "J/GiB", "dJ/GiB");
+  printf("%-16s %9s %9s %8s %8s %9s\n", "variant", "ms/GiB", "TB/s", "W(med)", "J/GiB", "dJ/GiB");
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
@@ -246,16 +255,19 @@ int main(int argc, char** argv) {
     CHK(hipEventElapsedTime(&ms, e0, e1));
     CHK(hipGetLastError());
     const double per_gib = ms / reps / (len / 1073741824.0);
-    printf("%-12s %9.4f %9.3f %8.1f %8.3f %9.3f\n", name, per_gib, 1.073741824 / per_gib, pw,
+    printf("%-16s %9.4f %9.3f %8.1f %8.3f %9.3f\n", name, per_gib, 1.073741824 / per_gib, pw,
            pw * per_gib / 1e3, (pw - idle) * per_gib / 1e3);
     fflush(stdout);
     std::this_thread::sleep_for(std::chrono::milliseconds(1000));  // cool down between variants
   };
   const int ncu = 256;
-  run("dma_copy", [&] { k_dma<true><<<ncu, 512>>>(d, nregions, o); });
-  run("dma_only", [&] { k_dma<false><<<ncu, 512>>>(d, nregions, o); });
+  run("dma_copy", [&] { k_dma<true, 1><<<ncu, 512>>>(d, nregions, o); });
+  run("dma_only", [&] { k_dma<false, 1><<<ncu, 512>>>(d, nregions, o); });
   run("reg_lane", [&] { k_reg<<<ncu, 512>>>(d, nregions, o); });
   run("coalesced", [&] { k_coalesced<<<ncu * 8, 256>>>((const u32x4*)d, len / 16, o); });
-  run("dma_copy", [&] { k_dma<true><<<ncu, 512>>>(d, nregions, o); });
+  run("dma_copy_pol0", [&] { k_dma<true, 0><<<ncu, 512>>>(d, nregions, o); });
+  run("dma_copy_sc1", [&] { k_dma<true, 2><<<ncu, 512>>>(d, nregions, o); });
+  run("dma_copy_sc01nt", [&] { k_dma<true, 3><<<ncu, 512>>>(d, nregions, o); });
+  run("dma_copy", [&] { k_dma<true, 1><<<ncu, 512>>>(d, nregions, o); });
   return 0;
 }
