@@ -358,23 +358,23 @@ extern "C" int dsx_get_stats(dsx_ctx_t* c, dsx_stats_t* out) {
 // roofline: the durations of exactly the launches its timed loop runs, with
 // no event between them).  Waits for the context's queued work first.
 extern "C" int dsx_stamps_begin(dsx_ctx_t* c, uint64_t max_launches) {
-  if (!c || max_launches == 0 || max_launches > (1ull << 24)) return DSX_E_INVAL;
+  if (!c || max_launches == 0 || max_launches > 65536) return DSX_E_INVAL;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->scan_stream != c->stream) HIPCHK(c, hipStreamSynchronize(c->scan_stream));
-  HIPCHK(c, grow(c, c->stamp_ring, max_launches * kStampWords));
-  std::vector<uint64_t> init(max_launches * kStampWords, 0ull);
-  for (uint64_t i = 0; i < max_launches; ++i) init[i * kStampWords] = ~0ull;  // t_first: a minimum
-  HIPCHK(c, hipMemcpy(c->stamp_ring.p, init.data(), init.size() * sizeof(uint64_t),
-                      hipMemcpyHostToDevice));
+  c->stamp_slots = (uint64_t)c->ncu * (uint64_t)c->scanl_waves;  // wave slots of a line scan
+  const uint64_t words = max_launches * c->stamp_slots * kStampWords;
+  HIPCHK(c, grow(c, c->stamp_ring, words));
+  HIPCHK(c, hipMemset(c->stamp_ring.p, 0, words * sizeof(uint64_t)));  // (end 0: slot unused)
   c->stamp_meta.clear();
   c->stamp_cap = max_launches;
   c->stamping = true;
   return DSX_OK;
 }
 
-// Stops stamping, waits for the stamped launches and copies min(cap, n)
-// records (in launch order) to out; *n = the launches stamped.
+// Stops stamping, waits for the stamped launches and reduces each one's
+// per-wave records (first start, last end, summed spans) into min(cap, n)
+// records in launch order; *n = the launches stamped.
 extern "C" int dsx_stamps_end(dsx_ctx_t* c, dsx_scan_stamp_t* out, uint64_t cap, uint64_t* n) {
   if (!c || !n || (cap && !out)) return DSX_E_INVAL;
   const bool was = c->stamping;
@@ -388,18 +388,24 @@ extern "C" int dsx_stamps_end(dsx_ctx_t* c, dsx_scan_stamp_t* out, uint64_t cap,
   *n = k;
   const uint64_t m = std::min(cap, k);
   if (!m) return DSX_OK;
-  std::vector<uint64_t> raw(m * kStampWords);
+  const uint64_t per = c->stamp_slots * kStampWords;
+  std::vector<uint64_t> raw(m * per);
   HIPCHK(c, hipMemcpy(raw.data(), c->stamp_ring.p, raw.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < m; ++i) {
-    const uint64_t* r = &raw[i * kStampWords];
     dsx_scan_stamp_t s{};
     s.seq = c->stamp_meta[i].first;
     s.bytes = c->stamp_meta[i].second;
-    s.t_first = r[0];
-    s.t_last = r[1];
-    s.wave_cycles = r[2];
-    s.wave_ticks = r[3];
-    s.waves = r[4];
+    s.t_first = ~0ull;
+    for (uint64_t w = 0; w < c->stamp_slots; ++w) {
+      const uint64_t* r = &raw[i * per + w * kStampWords];
+      if (r[1] == 0) continue;  // (no wave in this slot)
+      s.t_first = std::min(s.t_first, r[0]);
+      s.t_last = std::max(s.t_last, r[1]);
+      s.wave_ticks += r[1] - r[0];
+      s.wave_cycles += r[3] - r[2];
+      ++s.waves;
+    }
+    if (!s.waves) s.t_first = 0;
     out[i] = s;
   }
   return DSX_OK;
@@ -652,8 +658,8 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
                     : (uint32_t)(16 * (((uint64_t)kLine + delta - hmin) / 16));
   }
   c->last_grid_P = line ? P - delta : P;
-  if (c->stamping && line && c->stamp_meta.size() < c->stamp_cap) {
-    sa.stamp = c->stamp_ring.p + (uint64_t)kStampWords * c->stamp_meta.size();
+  if (c->stamping && line && c->stamp_meta.size() < c->stamp_cap && W == c->scanl_waves) {
+    sa.stamp = c->stamp_ring.p + c->stamp_slots * kStampWords * c->stamp_meta.size();
     c->stamp_meta.emplace_back(seq, len);
   }
   if (c->scan_trace && line) {
@@ -920,11 +926,12 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
     HIPCHK(c, hipGetLastError());
     return launch_publish(c, ta);
   }
-  if (c->fixup_fast && nseg <= 8 * 1024) {
+  if (c->fixup_fast && nseg <= 9 * 1024) {
     if (nseg <= 1024) hipLaunchKernelGGL(fixup_fast_kernel<1>, dim3(1), dim3(1024), 0, c->stream, ta);
     else if (nseg <= 2048) hipLaunchKernelGGL(fixup_fast_kernel<2>, dim3(1), dim3(1024), 0, c->stream, ta);
     else if (nseg <= 4096) hipLaunchKernelGGL(fixup_fast_kernel<4>, dim3(1), dim3(1024), 0, c->stream, ta);
-    else hipLaunchKernelGGL(fixup_fast_kernel<8>, dim3(1), dim3(1024), 0, c->stream, ta);
+    else if (nseg <= 8192) hipLaunchKernelGGL(fixup_fast_kernel<8>, dim3(1), dim3(1024), 0, c->stream, ta);
+    else hipLaunchKernelGGL(fixup_fast_kernel<9>, dim3(1), dim3(1024), 0, c->stream, ta);
   } else {
     hipLaunchKernelGGL(fixup_kernel, dim3(1), dim3(1024), 0, c->stream, ta);
   }

@@ -86,14 +86,14 @@ struct ScanArgs {
   const DevState* pub_state;
   HostState* pub_host;
   uint64_t pub_seq;
-  // measurement (dsx_stamps_begin): this launch's stamp record, or null.
-  // Every live wave adds its start/end (s_memrealtime, 100 MHz) and shader
-  // cycles (s_memtime) once, at its first and last instruction.
+  // measurement (dsx_stamps_begin): this launch's per-wave stamp records
+  // (kStampWords words per wave slot blockIdx.x * W + wave), or null.  Every
+  // wave writes its start/end s_memrealtime (100 MHz) and s_memtime (shader
+  // clock) once, taken at its first and last instruction.
   uint64_t* stamp;
 };
 
-// dsx_scan_stamp_t words the scan accumulates into (the host fills seq/bytes)
-constexpr int kStampWords = 8;  // t_first, t_last, wave_cycles, wave_ticks, waves, -, -, -
+constexpr int kStampWords = 4;  // per wave: start rt, end rt, start cycles, end cycles
 
 // line-aligned scan geometry: lane segments of S = 384*m bytes (3 DMA batches
 // of one 128-B line per lane, so the ring phase repeats), offsets in u16

@@ -29,7 +29,7 @@ template <int NT>
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
 template <int PER>
-__global__ void fixup_fast_kernel(StitchArgs a);
+__global__ void fixup_fast_kernel(StitchArgs a);  // PER = 1, 2, 4, 8, 9
 template <int PER>
 __global__ void finish_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);
@@ -258,8 +258,10 @@ struct dsx_ctx {
 
   dsx_stats_t stats{};
   // in-kernel stamps of the scan launches (dsx_stamps_begin .. dsx_stamps_end):
-  // record i (kStampWords words of stamp_ring) belongs to stamp_meta[i] = {seq, bytes}
+  // launch i's per-wave records (stamp_slots x kStampWords words from
+  // i * stamp_slots * kStampWords) belong to stamp_meta[i] = {seq, bytes}
   DevBuf<uint64_t> stamp_ring;
+  uint64_t stamp_slots = 0;
   bool stamping = false;
   uint64_t stamp_cap = 0;
   std::vector<std::pair<uint64_t, uint64_t>> stamp_meta;

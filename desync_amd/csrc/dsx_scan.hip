@@ -152,21 +152,28 @@ __device__ __forceinline__ void stamp_now(uint64_t& rt, uint64_t& cy) {
                : "memory");
 }
 
-// One live wave's share of its launch's stamp record (lane 0; vector
-// atomics).  The start half adds -t0 to the span sums and the end half +t1
-// (sums mod 2^64), so nothing stays live across the scan loop.
-__device__ __forceinline__ void stamp_wave(uint64_t* rec, bool end) {
+// A wave's stamp record {start realtime, end realtime, start cycles, end
+// cycles} (lane 0, plain stores into the wave slot's own record: a shared
+// record updated by atomics from every wave at the launch start serialised
+// in the L2 and delayed each wave's first line by ~100 us).  The start pair
+// waits in LDS meanwhile, so no register stays live across the scan.
+__device__ __forceinline__ void stamp_begin(uint64_t* s_stamp, uint32_t wave) {
   uint64_t rt, cy;
   stamp_now(rt, cy);
   if ((threadIdx.x & 63) == 0) {
-    if (end) {
-      atomicMax((unsigned long long*)&rec[1], (unsigned long long)rt);
-      atomicAdd((unsigned long long*)&rec[4], 1ull);
-    } else {
-      atomicMin((unsigned long long*)&rec[0], (unsigned long long)rt);
-    }
-    atomicAdd((unsigned long long*)&rec[2], (unsigned long long)(end ? cy : 0ull - cy));
-    atomicAdd((unsigned long long*)&rec[3], (unsigned long long)(end ? rt : 0ull - rt));
+    s_stamp[2 * wave] = rt;
+    s_stamp[2 * wave + 1] = cy;
+  }
+}
+__device__ __forceinline__ void stamp_end(uint64_t* rec, const uint64_t* s_stamp, uint32_t wave) {
+  uint64_t rt, cy;
+  stamp_now(rt, cy);
+  if ((threadIdx.x & 63) == 0) {
+    uint64_t* r = rec + (uint64_t)kStampWords * (blockIdx.x * (blockDim.x >> 6) + wave);
+    r[0] = s_stamp[2 * wave];
+    r[1] = rt;
+    r[2] = s_stamp[2 * wave + 1];
+    r[3] = cy;
   }
 }
 
@@ -682,7 +689,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
                                         : (a.trace ? __builtin_amdgcn_s_memrealtime() : 0);
   // in-kernel stamps of the launch (dsx_stamps_begin): every wave's first
   // instruction here, its last one at the end of its regions
-  if (a.stamp) stamp_wave(a.stamp, false);
+  __shared__ uint64_t s_stamp[2 * W];
+  if (a.stamp) stamp_begin(s_stamp, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 
   if (blockIdx.x == 0 && threadIdx.x < 8) a.queue_next[32 * threadIdx.x] = 0u;
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.pub_host)  // the previous piece's state
@@ -841,7 +849,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       a.trace ? a.trace + (uint64_t)kScanTraceWords * gridDim.x * W + 6ull * (blockIdx.x * W + wave)
               : nullptr;
   if (!live) {
-    if (a.stamp) stamp_wave(a.stamp, true);
+    if (a.stamp) stamp_end(a.stamp, s_stamp, wave);
 #if DSX_DIAG
   #if DSX_DIAG
   if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
@@ -1184,7 +1192,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     sh = nsh;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (a.stamp) stamp_wave(a.stamp, true);
+  if (a.stamp) stamp_end(a.stamp, s_stamp, wave);
   if (a.trace && lane == 0) {
     uint64_t* tr = a.trace + (uint64_t)kScanTraceWords * (blockIdx.x * W + wave);
     tr[4] = re_cyc;

@@ -694,6 +694,9 @@ template __global__ void fixup_fast_kernel<1>(StitchArgs);
 template __global__ void fixup_fast_kernel<2>(StitchArgs);
 template __global__ void fixup_fast_kernel<4>(StitchArgs);
 template __global__ void fixup_fast_kernel<8>(StitchArgs);
+// (an 8 GiB piece after the first: its stitch anchors max bytes before the
+// piece, so 8193 one-MiB segments)
+template __global__ void fixup_fast_kernel<9>(StitchArgs);
 
 // K3 + K4 over many workgroups, for pieces of at most kFinMaxSeg segments:
 // every workgroup loads all the SegInfo (40 B per segment, one round of global

@@ -329,7 +329,7 @@ typedef struct dsx_scan_stamp {
     uint64_t bytes;        /* bytes the launch scanned (one piece: <= 8 GiB) */
     uint64_t t_first, t_last;
     uint64_t wave_cycles, wave_ticks;
-    uint64_t waves;        /* waves that hashed at least one region */
+    uint64_t waves;        /* waves of the launch's grid */
     uint64_t reserved;
 } dsx_scan_stamp_t;
 int dsx_stamps_begin(dsx_ctx_t *ctx, uint64_t max_launches);

@@ -24,6 +24,10 @@ fi
 timeout -k 10 300 tools/power_sample.sh $OUT/power_bench.txt -- python3 $CMD > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 python3 tools/power_summary.py $OUT/power_bench.txt > $OUT/power_bench.json && cat $OUT/power_bench.json
+# the stamps' own cost: the same command without them, and once more with
+DSX_BENCH_STAMPS=0 timeout -k 10 200 python3 $CMD --no-cpu > $OUT/bench_nostamps.json 2> $OUT/bench_nostamps.err || { tail $OUT/bench_nostamps.err; exit 1; }
+timeout -k 10 200 python3 $CMD --no-cpu > $OUT/bench_2.json 2> $OUT/bench_2.err || { tail $OUT/bench_2.err; exit 1; }
+echo "no stamps: $(cat $OUT/bench_nostamps.json)"; echo "again: $(cat $OUT/bench_2.json)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $CMD > $OUT/trace_bench.json 2> $OUT/trace.err || { tail $OUT/trace.err; exit 1; }
 cat $OUT/trace_bench.json
 timeout -s KILL 180 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d $OUT/pmc_rdreq -o run --output-format csv -- python3 $CMD --no-cpu > $OUT/pmc_rdreq.json 2> $OUT/pmc_rdreq.err || { tail $OUT/pmc_rdreq.err; exit 1; }

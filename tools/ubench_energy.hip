@@ -25,6 +25,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <ctype.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -149,25 +151,24 @@ __global__ void k_coalesced(const u32x4* p, uint64_t n16, uint32_t* out) {
   if (acc == 0x12345678u) out[0] = acc;
 }
 
-// ---- board power: every hwmon power1_input, the busiest one reported -------
+// ---- board power of THIS GPU: the hwmon of HIP device 0's PCI function (the
+// box's other GPUs run other jobs: the busiest hwmon is not ours) ----------
 struct Sampler {
   std::vector<std::string> files;
   std::vector<std::vector<double>> w;  // per file, watts
   std::atomic<bool> run{false};
   std::thread th;
   Sampler() {
-    DIR* d = opendir("/sys/class/drm");
-    if (!d) return;
-    while (dirent* e = readdir(d)) {
-      if (strncmp(e->d_name, "card", 4) || strchr(e->d_name, '-')) continue;
-      std::string hw = std::string("/sys/class/drm/") + e->d_name + "/device/hwmon";
-      DIR* h = opendir(hw.c_str());
-      if (!h) continue;
-      while (dirent* f = readdir(h))
-        if (!strncmp(f->d_name, "hwmon", 5)) files.push_back(hw + "/" + f->d_name + "/power1_input");
-      closedir(h);
-    }
-    closedir(d);
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, 0) != hipSuccess) return;
+    for (char* p = bus; *p; ++p) *p = (char)tolower(*p);
+    std::string hw = std::string("/sys/bus/pci/devices/") + bus + "/hwmon";
+    DIR* h = opendir(hw.c_str());
+    if (!h) return;
+    while (dirent* f = readdir(h))
+      if (!strncmp(f->d_name, "hwmon", 5)) files.push_back(hw + "/" + f->d_name + "/power1_input");
+    closedir(h);
+    printf("power: %s\n", files.empty() ? "(no hwmon)" : files[0].c_str());
   }
   static double read1(const std::string& f) {
     FILE* fp = fopen(f.c_str(), "r");
