@@ -398,6 +398,7 @@ def main():
                 "kernel_ms": round(float(dur.mean()), 4),
                 "kernel_ms_min_max": [round(float(dur.min()), 4), round(float(dur.max()), 4)],
                 "clock_mhz": round(100.0 * cyc / tick, 1) if tick else None,
+                "wave_busy": round(float(np.mean([st.busy for st in stamps])), 4),
                 "scan_share_of_step": round(float(dur.sum()) / (dt * 1e3), 4),
                 "timing": "in-kernel s_memrealtime stamps of the timed jobs' scan launches",
             }

@@ -98,6 +98,13 @@ class ScanStamp(ctypes.Structure):
     def mhz(self):
         return 100.0 * self.wave_cycles / self.wave_ticks if self.wave_ticks else 0.0
 
+    @property
+    def busy(self):
+        """Mean fraction of the launch its waves were running (1 - the
+        wave-end spread and start skew)."""
+        span = self.t_last - self.t_first
+        return self.wave_ticks / (self.waves * span) if self.waves and span else 0.0
+
 
 class Seam(ctypes.Structure):
     _fields_ = [

@@ -47,6 +47,7 @@ def series(ctx, L, p, d_ptr, n, outs, cap, jobs, depth=4):
     st = ctx.stamps_end()
     base = st[0].t_first
     rows = [{"i": i, "t_ms": (s.t_first - base) / 1e5, "ms": s.ms, "mhz": round(s.mhz, 1),
+             "busy": round(s.busy, 4),
              "gbs": s.bytes / (s.ms / 1e3) / 1e9 if s.ms else 0.0,
              "gap_ms": ((s.t_first - st[i - 1].t_last) / 1e5) if i else 0.0}
             for i, s in enumerate(st)]
@@ -89,10 +90,10 @@ def main():
                    "after the series' first launch, gap_ms = idle before it"}
     for name, S in (("A (from idle)", A), ("B (after gap)", B)):
         print(f"== {name}: {S['jobs']} jobs, {S['gibs']:.1f} GiB/s wall")
-        print(f"{'i':>4} {'t_ms':>9} {'scan_ms':>8} {'MHz':>7} {'GB/s':>7} {'gap_ms':>7}")
+        print(f"{'i':>4} {'t_ms':>9} {'scan_ms':>8} {'MHz':>7} {'GB/s':>7} {'gap_ms':>7} {'busy':>6}")
         for r in S["launches"]:
             print(f"{r['i']:4d} {r['t_ms']:9.3f} {r['ms']:8.4f} {r['mhz']:7.1f} {r['gbs']:7.0f} "
-                  f"{r['gap_ms']:7.4f}")
+                  f"{r['gap_ms']:7.4f} {r['busy']:6.3f}")
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
