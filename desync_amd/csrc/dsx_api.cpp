@@ -193,6 +193,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
 
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
+  if (const char* v = getenv("DSX_TAIL_SPLIT")) c->tail_split = std::max(0, std::min(8, atoi(v)));
   if (const char* v = getenv("DSX_LANE_TARGET"))
     c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
   if (const char* v = getenv("DSX_INDEX_WINDOW")) c->index_window = (uint64_t)std::max(1L << 16, atol(v));
@@ -500,7 +501,22 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   }
   batches = line ? S / (3 * kLine) : (S / kRound + 1) / (uint32_t)cfgBR;
   const uint64_t region_bytes = 64ull * S;
-  const uint64_t nregions = len == 0 ? 0 : (span + region_bytes - 1) / region_bytes;
+  uint64_t nregions = len == 0 ? 0 : (span + region_bytes - 1) / region_bytes;
+  // Two region sizes (DSX_TAIL_SPLIT = k > 1, line scan, pieces of at least
+  // three big regions per wave slot): the last ~one big region's worth of
+  // bytes per wave slot is cut into regions with k times shorter lane
+  // segments, so the waves that drain the work queue last hold small regions
+  uint64_t nbig = nregions, S2 = 0;
+  if (line && !cc.dense && !cc.behind && c->tail_split > 1 && len > 0) {
+    const uint64_t m = S / (3 * kLine), m2 = std::max<uint64_t>(1, m / (uint64_t)c->tail_split);
+    const uint64_t tail = slots_total * region_bytes;
+    if (m2 < m && span >= 3 * tail) {
+      const uint64_t rb2 = 64ull * 3 * kLine * m2;
+      nbig = (span - tail) / region_bytes;
+      nregions = nbig + (span - nbig * region_bytes + rb2 - 1) / rb2;
+      S2 = 3 * kLine * m2;
+    }
+  }
   const uint64_t nlanes = nregions * 64;
   uint32_t rcap;
   if (cc.dense) {
@@ -513,6 +529,8 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   c->last_region_bytes = region_bytes;
   c->last_nregions = (uint32_t)nregions;
   c->last_region_cap = rcap;
+  c->last_nbig = (uint32_t)nbig;
+  c->last_region_bytes2 = S2 ? 64ull * S2 : 0;
   HIPCHK(c, grow(c, c->lane_slot, nlanes * LS));
   // region lists: the context's scratch, or (cc.keep: shards) buffers of
   // their own that outlive the call, so a re-walk can re-run the stitch
@@ -612,6 +630,11 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   sa.lane_bytes = S;
   sa.batches = batches;
   sa.nregions = (uint32_t)nregions;
+  if (S2) {
+    sa.nbig = (uint32_t)nbig;
+    sa.lane_bytes2 = (uint32_t)S2;
+    sa.batches2 = (uint32_t)(S2 / (3 * kLine));
+  }
   sa.region_cap = rcap;
   sa.tc = make_tc(p);
   sa.min_pos = cc.min_pos;
@@ -721,31 +744,32 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   } while (0)
 #if DSX_DIAG
 #define DSX_TRACE_VARIANTS(WV, SUB, D)                                                    \
-  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D, false>), g, b, 0, ss, sa); \
+  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D, false, false>), g, b, 0, ss, sa); \
   else if (c->variant == 6 && mode == 2)                                                  \
-    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D, false>), g, b, 0, ss, sa);         \
+    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D, false, false>), g, b, 0, ss, sa);         \
   else
 #else
 #define DSX_TRACE_VARIANTS(WV, SUB, D)
 #endif
-#define DSX_LAUNCHL(WV, SUB, D, FU)                                                       \
+#define DSX_LAUNCHL(WV, SUB, D, FU, TW)                                                   \
   do {                                                                                    \
     if (mode == 2)                                                                        \
-      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D, FU>), g, b, 0, ss, sa); \
+      hipLaunchKernelGGL((scanl_kernel<2, 0, WV, SUB, D, FU, TW>), g, b, 0, ss, sa);      \
     else if (mode == 1)                                                                   \
-      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D, FU>), g, b, 0, ss, sa); \
+      hipLaunchKernelGGL((scanl_kernel<1, 0, WV, SUB, D, FU, TW>), g, b, 0, ss, sa);      \
     else                                                                                  \
-      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D, FU>), g, b, 0, ss, sa); \
+      hipLaunchKernelGGL((scanl_kernel<0, 0, WV, SUB, D, FU, TW>), g, b, 0, ss, sa);      \
   } while (0)
 #if DSX_DIAG
     if (line && cc.behind) {
-      DSX_LAUNCHL(8, 8, 1, true);
+      DSX_LAUNCHL(8, 8, 1, true, false);
     } else
 #endif
     if (line) {
       DSX_ABLATEL(scanl_kernel, 8, 8, 1)
       DSX_TRACE_VARIANTS(8, 8, 1)
-      DSX_LAUNCHL(8, 8, 1, false);
+      if (sa.lane_bytes2) DSX_LAUNCHL(8, 8, 1, false, true);  // two region sizes
+      else DSX_LAUNCHL(8, 8, 1, false, false);
     } else {
 #if DSX_DIAG
       switch (c->scan_cfg) {
@@ -776,8 +800,10 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scan[par], 0));
   }
   PieceCands pc{};
-  pc.P = c->last_grid_P;  // region r covers (P' + r*RB, P' + (r+1)*RB]
+  pc.P = c->last_grid_P;  // region r covers (P' + base(r), P' + base(r) + bytes(r)]
   pc.RB = region_bytes;
+  pc.RB2 = c->last_region_bytes2;
+  pc.nbig = c->last_nbig;
   pc.nregions = (uint32_t)nregions;
   pc.region_cap = rcap;
   pc.region_cnt = rcnt;
@@ -1478,6 +1504,8 @@ static int shard_run(dsx_ctx* c, uint64_t entry, uint32_t rec_flags, bool rewalk
           PieceCands pc{};
           pc.P = c->last_grid_P;
           pc.RB = c->last_region_bytes;
+          pc.RB2 = c->last_region_bytes2;
+          pc.nbig = c->last_nbig;
           pc.nregions = c->last_nregions;
           pc.region_cap = c->last_region_cap;
           pc.region_cnt = cc.keep ? sh.kept[0].cnt.p : c->last_rcnt;

@@ -91,6 +91,13 @@ struct ScanArgs {
   // wave writes its start/end s_memrealtime (100 MHz) and s_memtime (shader
   // clock) once, taken at its first and last instruction.
   uint64_t* stamp;
+  // scanl_kernel, two region sizes: regions [nbig, nregions) have lane
+  // segments of lane_bytes2 bytes (batches2 trips) after the nbig regions of
+  // lane_bytes; lane_bytes2 == 0: one size
+  uint32_t nbig;
+  uint32_t lane_bytes2;
+  uint32_t batches2;
+  uint32_t pad3;
 };
 
 constexpr int kStampWords = 4;  // per wave: start rt, end rt, start cycles, end cycles

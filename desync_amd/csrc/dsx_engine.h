@@ -22,8 +22,8 @@ template <class H>
 __global__ void digest_pc_kernel(DigestArgs a);
 template <int MODE, int VARIANT, int BR, int NBUF, int W, int SUB, bool PF>
 __global__ void scan_kernel(ScanArgs a);
-template <int MODE, int VARIANT, int W, int SUB, int D, bool FUSE>
-__global__ void scanl_kernel(ScanArgs a);
+template <int MODE, int VARIANT, int W, int SUB, int D, bool FUSE, bool TWO>
+__global__ void scanl_kernel(ScanArgs a);  // TWO: two region sizes (ScanArgs.lane_bytes2)
 __global__ void stitch_task_kernel(TaskArgs b);
 template <int NT>
 __global__ void walk_kernel(StitchArgs a);
@@ -128,6 +128,7 @@ struct dsx_ctx {
   int digest_pc_chunks = 2;           // DSX_DIGEST_PC_CHUNKS: auto uses it up to this many chunks per grid lane
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
+  int tail_split = 0;                 // DSX_TAIL_SPLIT=k: tail regions with k x shorter lane segments
   uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
@@ -160,6 +161,8 @@ struct dsx_ctx {
   bool init_pending = false;     // next scan initialises DevState with init_carry
   uint64_t last_region_bytes = 0;  // geometry of the last enqueued piece's region lists
   uint32_t last_nregions = 0, last_region_cap = 0;
+  uint32_t last_nbig = 0;           // (two region sizes: regions [last_nbig, ...) have
+  uint64_t last_region_bytes2 = 0;  //  last_region_bytes2 bytes; 0: one size)
   uint64_t init_carry = 0;
   bool last_finish = false;  // the last stitch publishes its state (the host may poll)
   // a queued call's final state is published by the next scan's block 0

@@ -670,7 +670,7 @@ DSX_SCAN_INST_ALL(2, 1, 16, 4, false)
 // the grid has beyond the regions at once, the others once the regions run
 // out ("stitch behind the scan").
 // ---------------------------------------------------------------------------
-template <int MODE, int VARIANT, int W, int SUB, int D, bool FUSE>
+template <int MODE, int VARIANT, int W, int SUB, int D, bool FUSE, bool TWO>
 __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   constexpr int NC = kLine / 16;             // 16-B chunks per lane row
   constexpr int NI = kWave * kLine / 1024;   // DMA wave instructions per batch
@@ -719,10 +719,24 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   uint32_t my_prog = 0;
   const uint32_t stage_lds =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)stage);
-  const uint32_t S = a.lane_bytes;
-  const uint32_t M = a.batches;        // loop trips of 3 batches: S = 3*128*M
-  const uint32_t NB = 3u * M + 1u;     // batches per lane, warm-up line included
-  const uint64_t RB = 64ull * S;
+  // Two region sizes (a.lane_bytes2 != 0): regions [0, nbig) have lane
+  // segments of S1 bytes, the tail regions after them S2 < S1, so the waves
+  // that drain the work queue last hold small regions (a shorter tail).
+  // (TWO: a separate instantiation, since the second size's state costs the
+  // one-size loop SGPR spills)
+  auto region_base = [&](uint32_t r) -> uint64_t {  // grid-relative start of region r
+    if constexpr (TWO) {
+      return r <= a.nbig
+                 ? (uint64_t)r * 64u * a.lane_bytes
+                 : ((uint64_t)a.nbig * a.lane_bytes + (uint64_t)(r - a.nbig) * a.lane_bytes2) * 64u;
+    } else {
+      return (uint64_t)r * 64u * a.lane_bytes;
+    }
+  };
+  auto is_tail = [&](uint32_t r) -> bool {
+    if constexpr (TWO) return r >= a.nbig;
+    else return false;
+  };
 
   // DMA geometry: instruction i, lane j -> 16-B unit u = 64i + j of the wave's
   // 64 x 128 B image: row u/8, physical chunk u%8.  Row r stores logical
@@ -732,9 +746,17 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // row = 8i + (lane >> 3) and rot(row) = (4i + (lane >> 4)) % 8 depends on
   // i only through its parity: two per-lane bases, the rest is scalar
   static_assert(NC == 8 && NI == 8, "line DMA geometry");
-  const uint32_t dphys = lane & 7u;
-  const uint32_t dbase0 = (lane >> 3) * S + ((dphys + 8u - ((lane >> 4) & 7u)) & 7u) * 16u;
-  const uint32_t dbase1 = (lane >> 3) * S + ((dphys + 8u - ((4u + (lane >> 4)) & 7u)) & 7u) * 16u;
+  auto dbase_of = [&](uint32_t S, uint32_t parity) -> uint32_t {
+    const uint32_t dphys = lane & 7u;
+    return (lane >> 3) * S + ((dphys + 8u - ((4u * parity + (lane >> 4)) & 7u)) & 7u) * 16u;
+  };
+  // the current region's geometry (wave-uniform; changes at most once, when
+  // the wave moves on to the tail regions)
+  // S = 3*128*M; 3M+1 lines per lane (warm-up line).  Constant in the one-size
+  // instantiation (left mutable there the allocator spilled 10 more SGPRs)
+  using mut_u32 = std::conditional_t<TWO, uint32_t, const uint32_t>;
+  mut_u32 S = a.lane_bytes, M = a.batches;
+  mut_u32 dbase0 = dbase_of(a.lane_bytes, 0u), dbase1 = dbase_of(a.lane_bytes, 1u);
   const uint32_t rot = (lane >> 1) % (uint32_t)NC;
   TestConsts tcv = a.tc;
   asm volatile("" : "+v"(tcv.c0));
@@ -745,7 +767,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   // readable bytes; offsets below the base wrap out of range and read 0.
   auto desc_of = [&](uint32_t region, u32x4& rsrc, uint32_t& sh) {
     sh = region == 0 ? a.shift0 : 0u;
-    const int64_t rel = (int64_t)region * (int64_t)RB - (int64_t)a.delta - kLine + (int64_t)sh;
+    const int64_t rel = (int64_t)region_base(region) - (int64_t)a.delta - kLine + (int64_t)sh;
     const uint64_t rp = (uint64_t)(uintptr_t)(a.base + rel);
     const uint64_t nrec64 = (uint64_t)((int64_t)a.len - rel);
     const uint32_t nrec = nrec64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nrec64;
@@ -756,6 +778,26 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   };
   // batch b of every lane (b = 0: warm-up line); b >= NB: out-of-range loads
   // (zeros) so every batch is NI instructions
+  // (issue_in: a line of a region with lane segments rS and DMA bases d0/d1,
+  // or zero loads if !ok -- the first line of the first tail region, TWO)
+  auto issue_in = [&](const u32x4& rsrc, uint32_t sh, uint32_t b, bool ok, uint32_t rS,
+                      uint32_t d0, uint32_t d1) {
+    if constexpr (VARIANT == 4) return;
+    const uint32_t sb = b * (uint32_t)kLine - sh;  // scalar part
+    uint32_t vo[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      uint32_t ssum = (uint32_t)i * 8u * rS + sb;
+      asm volatile("" : "+s"(ssum));
+      vo[i] = ok ? ((i & 1) ? d1 : d0) + ssum : 0xFFFFFFF0u;
+    }
+    switch (a.nt_loads) {
+      case 1: dma16x8<1>(rsrc, vo, stage_lds); break;
+      case 2: dma16x8<2>(rsrc, vo, stage_lds); break;
+      case 3: dma16x8<3>(rsrc, vo, stage_lds); break;
+      default: dma16x8<0>(rsrc, vo, stage_lds); break;
+    }
+  };
   auto issue = [&](const u32x4& rsrc, uint32_t sh, uint32_t b) {
     if constexpr (VARIANT == 4) return;
     const uint32_t sb = b * (uint32_t)kLine - sh;  // scalar part
@@ -765,7 +807,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       // the opaque scalar sum keeps LICM from hoisting 8 per-lane offsets
       uint32_t ssum = (uint32_t)i * 8u * S + sb;
       asm volatile("" : "+s"(ssum));
-      vo[i] = (b < NB) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
+      vo[i] = (b < 3u * M + 1u) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
     }
     switch (a.nt_loads) {
       case 1: dma16x8<1>(rsrc, vo, stage_lds); break;
@@ -811,6 +853,14 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   u32x4 rsrc = {0u, 0u, 0u, 0u};
   uint32_t sh = 0;
   if (live) {
+    if constexpr (TWO) {
+      if (is_tail(region)) {  // (a grid with more wave slots than big regions)
+        S = a.lane_bytes2;
+        M = a.batches2;
+        dbase0 = dbase_of(S, 0u);
+        dbase1 = dbase_of(S, 1u);
+      }
+    }
     desc_of(region, rsrc, sh);
     issue(rsrc, sh, 0u);
   }
@@ -965,11 +1015,17 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         __builtin_amdgcn_s_setprio(0);
       else
         __builtin_amdgcn_s_setprio(1);
-      if (b + 1u < NB) {
+      if (b + 1u < 3u * M + 1u) {
         issue(rsrc, sh, b + 1u);
       } else {
         resolve_next();
-        issue(nrsrc, nsh, next < a.nregions ? 0u : NB);
+        if (TWO && next < a.nregions && is_tail(next) && S != a.lane_bytes2) {
+          // the first tail region: its own lane geometry
+          const uint32_t S2 = a.lane_bytes2;
+          issue_in(nrsrc, nsh, 0u, true, S2, dbase_of(S2, 0u), dbase_of(S2, 1u));
+        } else {
+          issue(nrsrc, nsh, next < a.nregions ? 0u : 3u * M + 1u);
+        }
       }
       if constexpr (VARIANT == 5) dma_issue += __builtin_amdgcn_s_memtime() - tw2;
     };
@@ -1138,7 +1194,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     // ---- region end: compact the lanes' hits into one sorted region list ----
     // valid cut offsets o: piece-relative p = lane_p + o in [1, len] and
     // absolute p >= min_pos (windows reaching before the chain origin)
-    const int64_t lane_p = (int64_t)region * (int64_t)RB + (int64_t)lane * S - (int64_t)a.delta;
+    const int64_t lane_p = (int64_t)region_base(region) + (int64_t)lane * S - (int64_t)a.delta;
     int64_t lo = 1 - lane_p;
     const int64_t lo2 = (int64_t)a.min_pos - (int64_t)a.piece_abs - lane_p;
     lo = lo > lo2 ? lo : lo2;
@@ -1190,6 +1246,14 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     region = next;
     rsrc = nrsrc;
     sh = nsh;
+    if constexpr (TWO) {
+      if (is_tail(region) && S != a.lane_bytes2) {  // into the tail regions (once)
+        S = a.lane_bytes2;
+        M = a.batches2;
+        dbase0 = dbase_of(S, 0u);
+        dbase1 = dbase_of(S, 1u);
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (a.stamp) stamp_end(a.stamp, s_stamp, wave);
@@ -1214,20 +1278,23 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 }
 
 #define DSX_SCANL_INST(W, SUB, D)                                          \
-  template __global__ void scanl_kernel<0, 0, W, SUB, D, false>(ScanArgs); \
-  template __global__ void scanl_kernel<1, 0, W, SUB, D, false>(ScanArgs); \
-  template __global__ void scanl_kernel<2, 0, W, SUB, D, false>(ScanArgs);
+  template __global__ void scanl_kernel<0, 0, W, SUB, D, false, false>(ScanArgs); \
+  template __global__ void scanl_kernel<1, 0, W, SUB, D, false, false>(ScanArgs); \
+  template __global__ void scanl_kernel<2, 0, W, SUB, D, false, false>(ScanArgs); \
+  template __global__ void scanl_kernel<0, 0, W, SUB, D, false, true>(ScanArgs);  \
+  template __global__ void scanl_kernel<1, 0, W, SUB, D, false, true>(ScanArgs);  \
+  template __global__ void scanl_kernel<2, 0, W, SUB, D, false, true>(ScanArgs);
 #if DSX_DIAG
 // the stitch behind the scan (DSX_FUSE=1): diagnostic build only
-template __global__ void scanl_kernel<0, 0, 8, 8, 1, true>(ScanArgs);
-template __global__ void scanl_kernel<1, 0, 8, 8, 1, true>(ScanArgs);
-template __global__ void scanl_kernel<2, 0, 8, 8, 1, true>(ScanArgs);
-template __global__ void scanl_kernel<2, 1, 8, 8, 1, false>(ScanArgs);
-template __global__ void scanl_kernel<2, 3, 8, 8, 1, false>(ScanArgs);
-template __global__ void scanl_kernel<2, 4, 8, 8, 1, false>(ScanArgs);
-template __global__ void scanl_kernel<2, 5, 8, 8, 1, false>(ScanArgs);
-template __global__ void scanl_kernel<2, 6, 8, 8, 1, false>(ScanArgs);
-template __global__ void scanl_kernel<2, 7, 8, 8, 1, false>(ScanArgs);
+template __global__ void scanl_kernel<0, 0, 8, 8, 1, true, false>(ScanArgs);
+template __global__ void scanl_kernel<1, 0, 8, 8, 1, true, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 0, 8, 8, 1, true, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 1, 8, 8, 1, false, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 3, 8, 8, 1, false, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 4, 8, 8, 1, false, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 5, 8, 8, 1, false, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 6, 8, 8, 1, false, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 7, 8, 8, 1, false, false>(ScanArgs);
 #endif
 DSX_SCANL_INST(8, 8, 1)  // D = 2 needs 16 more VGPRs than the 256 of two waves per SIMD
 

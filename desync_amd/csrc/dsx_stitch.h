@@ -9,14 +9,29 @@ namespace dsx {
 // scan.  Region r covers positions (P + r*RB, P + (r+1)*RB]; candidate =
 // P + r*RB + list entry.
 struct PieceCands {
-  uint64_t P;             // absolute position of the piece's first byte
-  uint64_t RB;            // region bytes (64 * lane segment)
+  uint64_t P;             // absolute position of the region grid's origin
+  uint64_t RB;            // region bytes (64 * lane segment) of regions [0, nbig)
   uint32_t nregions;
   uint32_t region_cap;
   const uint32_t* region_cnt;
   const uint32_t* region_list;
   const uint32_t* overflow;
+  uint64_t RB2;           // region bytes of the tail regions [nbig, nregions); 0: one size
+  uint32_t nbig;
+  uint32_t pad;
 };
+
+// Region r covers grid-relative positions (base(r), base(r) + bytes(r)].
+__host__ __device__ __forceinline__ uint64_t pc_region_base(const PieceCands& pc, uint64_t r) {
+  return (pc.RB2 == 0 || r <= pc.nbig) ? r * pc.RB
+                                       : (uint64_t)pc.nbig * pc.RB + (r - pc.nbig) * pc.RB2;
+}
+// the region whose bytes hold grid-relative offset x, i.e. the first region
+// with base(r) + bytes(r) > x (may be >= nregions past the end)
+__host__ __device__ __forceinline__ uint64_t pc_region_of(const PieceCands& pc, uint64_t x) {
+  const uint64_t big = (uint64_t)pc.nbig * pc.RB;
+  return (pc.RB2 == 0 || x < big) ? x / pc.RB : pc.nbig + (x - big) / pc.RB2;
+}
 
 // Chain rule inputs (chunker.go:206-277): L is the blob length (known only on
 // the final piece), PE the absolute end of the scanned bytes.

@@ -71,8 +71,8 @@ struct GlobalSrc {
   __device__ uint64_t first_in(uint64_t a, uint64_t b) const {
     if (b <= pc->P) return kNone;
     const uint64_t pos = a < pc->P ? pc->P : a;
-    for (uint64_t r = (pos - pc->P) / pc->RB; r < pc->nregions; ++r) {
-      const uint64_t base = pc->P + r * pc->RB;  // region covers (base, base + RB]
+    for (uint64_t r = pc_region_of(*pc, pos - pc->P); r < pc->nregions; ++r) {
+      const uint64_t base = pc->P + pc_region_base(*pc, r);  // region covers (base, base + bytes]
       if (base >= b) break;
       const uint32_t cnt = pc->region_cnt[r];
       const uint32_t n = cnt < pc->region_cap ? cnt : pc->region_cap;
@@ -188,8 +188,8 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
   const PieceCands& pc = a.pc;
 
   // ---- gather candidates in (lo, hi] into LDS, sorted (region order) ----
-  const uint64_t r0 = lo <= pc.P ? 0 : (lo - pc.P) / pc.RB;
-  uint64_t r1 = hi <= pc.P ? 0 : (hi - pc.P - 1) / pc.RB + 1;  // exclusive
+  const uint64_t r0 = lo <= pc.P ? 0 : pc_region_of(pc, lo - pc.P);
+  uint64_t r1 = hi <= pc.P ? 0 : pc_region_of(pc, hi - pc.P - 1) + 1;  // exclusive
   if (r1 > pc.nregions) r1 = pc.nregions;
   const uint32_t nreg = r1 > r0 ? (uint32_t)(r1 - r0) : 0u;
   bool dense = nreg > kWalkMaxRegions;
@@ -222,7 +222,8 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
         if (s_off[m] <= g) l = m; else h = m;
       }
       const uint64_t r = r0 + l;
-      const uint64_t p = pc.P + r * pc.RB + pc.region_list[r * (uint64_t)pc.region_cap + (g - s_off[l])];
+      const uint64_t p = pc.P + pc_region_base(pc, r) +
+                         pc.region_list[r * (uint64_t)pc.region_cap + (g - s_off[l])];
       // keep the array sorted: below-range -> 0, above-range -> UINT32_MAX
       cand[g] = p <= lo ? 0u : (p > hi ? 0xFFFFFFFFu : (uint32_t)(p - lo));
     }
@@ -940,9 +941,9 @@ __global__ __launch_bounds__(64) void seam_cands_kernel(PieceCands pc, uint64_t 
   const uint32_t lane = threadIdx.x;
   constexpr uint32_t kMax = DSX_SEAM_MAX_CANDS;
   uint32_t n = 0;  // wave-uniform
-  const uint64_t r0 = lo > pc.P ? (lo - pc.P) / pc.RB : 0;
+  const uint64_t r0 = lo > pc.P ? pc_region_of(pc, lo - pc.P) : 0;
   for (uint64_t r = r0; r < pc.nregions && n <= kMax; ++r) {
-    const uint64_t base = pc.P + r * pc.RB;  // region covers (base, base + RB]
+    const uint64_t base = pc.P + pc_region_base(pc, r);  // region covers (base, base + bytes]
     if (base >= wend) break;
     const uint32_t cnt0 = pc.region_cnt[r];
     const uint32_t cnt = cnt0 < pc.region_cap ? cnt0 : pc.region_cap;

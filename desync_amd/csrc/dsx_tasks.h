@@ -43,8 +43,8 @@ __device__ __attribute__((noinline)) void walk_task(const WalkJob& jr, uint32_t 
 
   // ---- the candidates in (lo, hi], sorted, into LDS: per batch of 16
   // regions one round of loads (counts and the first 64 entries of each) ----
-  const uint64_t r0 = lo <= pc.P ? 0 : (lo - pc.P) / pc.RB;
-  uint64_t r1 = hi <= pc.P ? 0 : (hi - pc.P - 1) / pc.RB + 1;  // exclusive
+  const uint64_t r0 = lo <= pc.P ? 0 : pc_region_of(pc, lo - pc.P);
+  uint64_t r1 = hi <= pc.P ? 0 : pc_region_of(pc, hi - pc.P - 1) + 1;  // exclusive
   if (r1 > pc.nregions) r1 = pc.nregions;
   const uint32_t nreg = r1 > r0 ? (uint32_t)(r1 - r0) : 0u;
   uint32_t total = 0;
@@ -78,7 +78,7 @@ __device__ __attribute__((noinline)) void walk_task(const WalkJob& jr, uint32_t 
       if ((uint32_t)i >= nr) continue;  // (not break: the loop stays unrolled)
       const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, i);
       const uint32_t o = total + (uint32_t)__builtin_amdgcn_readlane((int)excl, i);
-      const uint64_t rp = pc.P + (rbase + i) * pc.RB;
+      const uint64_t rp = pc.P + pc_region_base(pc, rbase + i);
       auto put = [&](uint32_t idx, uint32_t ent) {
         const uint64_t p = rp + ent;
         cand[o + idx] = p <= lo ? 0u : (p > hi ? 0xFFFFFFFFu : (uint32_t)(p - lo));

@@ -108,19 +108,29 @@ def test_config4_64gib_zeros(dctx):
     _free()
 
 
-@pytest.mark.parametrize("params", [(MIN, AVG, MAX), (4096, 16384, 65536)])
-def test_uniform_9gib_two_pieces(dctx, params):
+@pytest.mark.parametrize("params,tail", [((MIN, AVG, MAX), 0), ((4096, 16384, 65536), 0),
+                                         ((MIN, AVG, MAX), 4), ((4096, 16384, 65536), 4)])
+def test_uniform_9gib_two_pieces(dctx, monkeypatch, params, tail):
     """> 2^32 bytes and two 8 GiB pieces: the carried chain state, 64-bit
-    offsets and the second piece's region grid, cut for cut."""
+    offsets and the second piece's region grid, cut for cut.  tail = 4
+    (DSX_TAIL_SPLIT): the 8 GiB piece's last regions have 4x shorter lane
+    segments (two region sizes in the scan and the stitch)."""
     import torch
     import desync_amd
+    from desync_amd import _lib
+    ctx = dctx
+    if tail:
+        monkeypatch.setenv("DSX_TAIL_SPLIT", str(tail))
+        ctx = _lib.Context(0)
     n = 9 * GiB + 12345
     t = torch.empty(n, dtype=torch.uint8, device="cuda")
-    _gen(dctx, t, 0, n, "uniform", 7)
+    _gen(ctx, t, 0, n, "uniform", 7)
     host = t.cpu().numpy()
-    if params == (MIN, AVG, MAX):
+    if params == (MIN, AVG, MAX) and not tail:
         _check_bytes(host, 0, "uniform", 7)
-    got = desync_amd.cut_device(t.data_ptr(), n, *params, ctx=dctx)
+    got = desync_amd.cut_device(t.data_ptr(), n, *params, ctx=ctx)
+    if tail:
+        ctx.close()
     del t
     _free()
     ref = o.chunk_parallel(host, *params, o.default_threads())
