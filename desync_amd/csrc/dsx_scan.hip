@@ -1019,10 +1019,12 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         issue(rsrc, sh, b + 1u);
       } else {
         resolve_next();
-        if (TWO && next < a.nregions && is_tail(next) && S != a.lane_bytes2) {
-          // the first tail region: its own lane geometry
-          const uint32_t S2 = a.lane_bytes2;
-          issue_in(nrsrc, nsh, 0u, true, S2, dbase_of(S2, 0u), dbase_of(S2, 1u));
+        const uint32_t nS = (TWO && next < a.nregions)
+                                ? (is_tail(next) ? a.lane_bytes2 : a.lane_bytes) : S;
+        if (TWO && nS != S) {
+          // the next region has the other lane geometry (the first tail region,
+          // or a big one stolen from a slower XCD's counter after it)
+          issue_in(nrsrc, nsh, 0u, true, nS, dbase_of(nS, 0u), dbase_of(nS, 1u));
         } else {
           issue(nrsrc, nsh, next < a.nregions ? 0u : 3u * M + 1u);
         }
@@ -1247,9 +1249,13 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     rsrc = nrsrc;
     sh = nsh;
     if constexpr (TWO) {
-      if (is_tail(region) && S != a.lane_bytes2) {  // into the tail regions (once)
-        S = a.lane_bytes2;
-        M = a.batches2;
+      // the region's lane geometry (tail or big: a wave whose XCD counter ran
+      // dry can steal a big region after tail ones)
+      const bool tl = is_tail(region);
+      const uint32_t nS = tl ? a.lane_bytes2 : a.lane_bytes;
+      if (nS != S) {
+        S = nS;
+        M = tl ? a.batches2 : a.batches;
         dbase0 = dbase_of(S, 0u);
         dbase1 = dbase_of(S, 1u);
       }
