@@ -723,10 +723,10 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__>), g, b, 0, ss, sa); \
   else
 #define DSX_ABLATEL(K, ...)                                                                \
-  if (c->variant == 1) hipLaunchKernelGGL((K<2, 1, __VA_ARGS__, false>), g, b, 0, ss, sa); \
-  else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__, false>), g, b, 0, ss, sa); \
-  else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__, false>), g, b, 0, ss, sa); \
-  else if (c->variant == 7 && mode == 2) hipLaunchKernelGGL((K<2, 7, __VA_ARGS__, false>), g, b, 0, ss, sa); \
+  if (c->variant == 1) hipLaunchKernelGGL((K<2, 1, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
+  else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
+  else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
+  else if (c->variant == 7 && mode == 2) hipLaunchKernelGGL((K<2, 7, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
   else
 #else
 #define DSX_ABLATE(K, ...)
