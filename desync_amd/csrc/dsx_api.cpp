@@ -193,7 +193,9 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
 
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
+  if (const char* v = getenv("DSX_DIGEST_PF")) c->digest_pf = atoi(v) != 0;
   if (const char* v = getenv("DSX_TAIL_SPLIT")) c->tail_split = std::max(0, std::min(8, atoi(v)));
+  if (const char* v = getenv("DSX_TAIL_MULT")) c->tail_mult = std::max(1, std::min(4, atoi(v)));
   if (const char* v = getenv("DSX_LANE_TARGET"))
     c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
   if (const char* v = getenv("DSX_INDEX_WINDOW")) c->index_window = (uint64_t)std::max(1L << 16, atol(v));
@@ -502,14 +504,18 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   batches = line ? S / (3 * kLine) : (S / kRound + 1) / (uint32_t)cfgBR;
   const uint64_t region_bytes = 64ull * S;
   uint64_t nregions = len == 0 ? 0 : (span + region_bytes - 1) / region_bytes;
-  // Two region sizes (DSX_TAIL_SPLIT = k > 1, line scan, pieces of at least
-  // three big regions per wave slot): the last ~one big region's worth of
-  // bytes per wave slot is cut into regions with k times shorter lane
+  // Two region sizes (DSX_TAIL_SPLIT = k > 1, default 3; line scan, pieces of
+  // at least three big regions per wave slot): the last ~one big region's
+  // worth of bytes per wave slot is cut into regions with k times shorter lane
   // segments, so the waves that drain the work queue last hold small regions
+  // (DSX_TAIL_MULT = j: j big regions' worth per wave slot).  On the 8 GiB
+  // pieces the waves end together (wave_busy 0.947 -> 0.98) and the scan is
+  // 1 % faster; k = 4 the same with more warm-up lines (HBM reads 1.021 x the
+  // input against 1.014), k = 2, 8 and j = 2 less (profiles/r04d, r04e, r04g)
   uint64_t nbig = nregions, S2 = 0;
   if (line && !cc.dense && !cc.behind && c->tail_split > 1 && len > 0) {
     const uint64_t m = S / (3 * kLine), m2 = std::max<uint64_t>(1, m / (uint64_t)c->tail_split);
-    const uint64_t tail = slots_total * region_bytes;
+    const uint64_t tail = slots_total * region_bytes * (uint64_t)c->tail_mult;
     if (m2 < m && span >= 3 * tail) {
       const uint64_t rb2 = 64ull * 3 * kLine * m2;
       nbig = (span - tail) / region_bytes;
@@ -1308,16 +1314,25 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
     return DSX_OK;
   }
   // Lanes: exactly the workgroups that are resident at once (occupancy is set
-  // by VGPRs: 2 per CU for SHA-512, 3 for SHA-256), every lane pulling chunks
+  // by VGPRs: 2 per CU for SHA-512, 3 without the prefetch, 4 for SHA-256),
+  // every lane pulling chunks
   // from the queue.  A larger grid would hand its non-resident workgroups a
   // static share that starts only when the first wave of workgroups is done.
   int per_cu = 0;
-  if (algo == DSX_DIGEST_SHA512_256)
-    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha512>,
-                                                           kDigestThreads, 0));
-  else
-    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, digest_kernel<Sha256>,
-                                                           kDigestThreads, 0));
+  const bool sha512 = algo == DSX_DIGEST_SHA512_256;
+#if DSX_DIAG
+  const bool pf = c->digest_pf != 0;
+#else
+  constexpr bool pf = true;
+#endif
+  const void* kern = sha512 ? (const void*)digest_kernel<Sha512, true>
+                            : (const void*)digest_kernel<Sha256, true>;
+#if DSX_DIAG
+  if (!pf)
+    kern = sha512 ? (const void*)digest_kernel<Sha512, false>
+                  : (const void*)digest_kernel<Sha256, false>;
+#endif
+  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kDigestThreads, 0));
   if (per_cu < 1) per_cu = 1;
   const uint64_t blocks = std::max<uint64_t>(
       1, std::min<uint64_t>((max_n + kDigestThreads - 1) / kDigestThreads,
@@ -1325,9 +1340,11 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
   HIPCHK(c, hipMemsetAsync(queue, 0, 4, stream));
   da.queue = queue;
   da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * kDigestThreads);
-  // more chunks than lanes: the queue hands them out longest first (a
-  // counting sort by size class, three small passes on the same stream)
-  if (own && c->digest_lpt && max_n > blocks * kDigestThreads && max_n < (1ull << 32)) {
+  // the chunks go out longest first (a counting sort by size class, three
+  // small passes on the same stream): with more chunks than lanes the long
+  // chains start in the first round; with fewer, each wave's 64 static chunks
+  // are of one size, so no lane idles behind a longer neighbour
+  if (own && c->digest_lpt && max_n >= 8u * kDigestThreads && max_n < (1ull << 32)) {
     HIPCHK(c, grow(c, c->dg_order, max_n));
     HIPCHK(c, c->dg_cls.ensure(2 * kSizeClasses));
     HIPCHK(c, hipMemsetAsync(c->dg_cls.p, 0, kSizeClasses * sizeof(uint32_t), stream));
@@ -1340,12 +1357,20 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
     HIPCHK(c, hipGetLastError());
     da.order = c->dg_order.p;
   }
-  if (algo == DSX_DIGEST_SHA512_256)
-    hipLaunchKernelGGL(digest_kernel<Sha512>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
-                       stream, da);
+  if (sha512 && pf)
+    hipLaunchKernelGGL((digest_kernel<Sha512, true>), dim3((uint32_t)blocks), dim3(kDigestThreads),
+                       0, stream, da);
+  else if (pf)
+    hipLaunchKernelGGL((digest_kernel<Sha256, true>), dim3((uint32_t)blocks), dim3(kDigestThreads),
+                       0, stream, da);
+#if DSX_DIAG
+  else if (sha512)
+    hipLaunchKernelGGL((digest_kernel<Sha512, false>), dim3((uint32_t)blocks), dim3(kDigestThreads),
+                       0, stream, da);
   else
-    hipLaunchKernelGGL(digest_kernel<Sha256>, dim3((uint32_t)blocks), dim3(kDigestThreads), 0,
-                       stream, da);
+    hipLaunchKernelGGL((digest_kernel<Sha256, false>), dim3((uint32_t)blocks), dim3(kDigestThreads),
+                       0, stream, da);
+#endif
   HIPCHK(c, hipGetLastError());
   return DSX_OK;
 }

@@ -545,7 +545,11 @@ __global__ __launch_bounds__(256) void digest_order_scatter_kernel(DigestArgs a,
   }
 }
 
-template <class H>
+// PF: prefetch the next full block of the chunk while the current one is
+// compressed (its 36-dword window stays live across the compression: SHA-512
+// 201 VGPRs, 2 waves per SIMD).  Without it SHA-512 fits 3 waves per SIMD
+// (165 VGPRs), and is slower all the same (diagnostic build only).
+template <class H, bool PF>
 __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
   constexpr int BLK = H::BLK;
   const uint32_t lane = threadIdx.x & 63u;
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
         }
         pos += BLK;
         // prefetch the next full block of this chunk
-        have_next = e - pos >= (uint64_t)BLK && fast_ok<BLK>(pos, a.len);
+        have_next = PF && e - pos >= (uint64_t)BLK && fast_ok<BLK>(pos, a.len);
         if (have_next) fetch_raw<BLK>(a.blob, pos, raw);
       } else {
         const uint64_t bits = (e - s) * 8u;
@@ -650,8 +654,14 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
   }
 }
 
-template __global__ void digest_kernel<Sha512>(DigestArgs);
-template __global__ void digest_kernel<Sha256>(DigestArgs);
+template __global__ void digest_kernel<Sha512, true>(DigestArgs);
+template __global__ void digest_kernel<Sha256, true>(DigestArgs);
+#if DSX_DIAG
+// without the prefetch (DSX_DIGEST_PF=0): 3 waves per SIMD for SHA-512, and
+// 11-13 % slower at 4-16 GiB (profiles/r04e)
+template __global__ void digest_kernel<Sha512, false>(DigestArgs);
+template __global__ void digest_kernel<Sha256, false>(DigestArgs);
+#endif
 
 // ---------------------------------------------------------------------------
 // digest_pc_kernel -- the same IDs with each chunk's work split over two waves.

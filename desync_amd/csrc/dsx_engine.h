@@ -16,7 +16,7 @@
 #include "dsx_stitch.h"
 
 namespace dsx {
-template <class H>
+template <class H, bool PF>
 __global__ void digest_kernel(DigestArgs a);
 template <class H>
 __global__ void digest_pc_kernel(DigestArgs a);
@@ -128,7 +128,8 @@ struct dsx_ctx {
   int digest_pc_chunks = 2;           // DSX_DIGEST_PC_CHUNKS: auto uses it up to this many chunks per grid lane
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
-  int tail_split = 0;                 // DSX_TAIL_SPLIT=k: tail regions with k x shorter lane segments
+  int tail_split = 3;                 // DSX_TAIL_SPLIT=k: tail regions with k x shorter lane segments (0/1: one size)
+  int tail_mult = 1;                  // DSX_TAIL_MULT=j: the split tail is j big regions per wave slot
   uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
@@ -155,6 +156,7 @@ struct dsx_ctx {
   DevBuf<uint32_t> dg_order;  // chunk IDs: longest-first queue order (ctx-stream launches)
   DevBuf<uint32_t> dg_cls;    // chunk IDs: [kSizeClasses] counts, [kSizeClasses] offsets
   int digest_lpt = 1;         // DSX_DIGEST_LPT=0: digest_kernel's queue in index order
+  int digest_pf = 1;          // DSX_DIGEST_PF=0: digest_kernel without the block prefetch
   DevBuf<DevState> state;
   HostState* h_state = nullptr;  // pinned mirror published by fixup_kernel
   uint64_t piece_seq = 0;        // global piece counter (overflow parity, freshness)

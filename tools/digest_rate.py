@@ -45,6 +45,14 @@ def main():
             row[name + "_gibs"] = st["gibs_median"]
             row[name + "_ms"] = round(st["s_median"] * 1e3, 3)
             row[name] = st
+            # the C call alone: IDs into a preallocated host array, no Python list
+            e64 = np.ascontiguousarray(ends, dtype=np.uint64)
+            raw = np.empty((e64.size, 32), dtype=np.uint8)
+            sc, _ = repeat(lambda: _lib.check(L.dsx_chunk_ids(
+                ctx.h, ctypes.c_void_p(t.data_ptr()), n, 0, e64.ctypes.data, e64.size,
+                raw.ctypes.data, 0, algo), ctx.h), n)
+            row[name + "_call_gibs"] = sc["gibs_median"]
+            row[name + "_call"] = sc
             # spot-check a few IDs against hashlib
             starts = np.concatenate([[0], ends[:-1]])
             for i in (0, ends.size // 2, ends.size - 1):
@@ -56,7 +64,7 @@ def main():
         del t
         torch.cuda.empty_cache()
     print(json.dumps({"tool": "digest_rate", "params": "16/64/256 KiB", "rows": rows,
-                      "note": "wall time of dsx_chunk_ids incl. sync and 32 B/chunk D2H; blob resident"}))
+                      "note": "<algo>_gibs: make.chunk_ids wall time (the C call + the Python list of IDs); <algo>_call_gibs: dsx_chunk_ids alone incl. sync and 32 B/chunk D2H; blob resident"}))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-4 closing profile on the final defaults (two region sizes, longest-
+# first chunk IDs): the GPU suite; the driver's command with board power, again
+# without the stamps, under rocprofv3 --kernel-trace --stats, with the L2
+# read-request counters and with GRBM_GUI_ACTIVE / SQ_BUSY_CYCLES; configs 3
+# and 4 at full size; chunk-ID, IndexFromFile / VerifyIndex and host rates.
+# Outputs under gpurun_out/$TAG/.
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${1:-r04f}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+CMD="bench.py --gpus 1 --steps 20 --warmup 5"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 300 tools/power_sample.sh $OUT/power_bench.txt -- python3 $CMD > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+python3 tools/power_summary.py $OUT/power_bench.txt > $OUT/power_bench.json && cat $OUT/power_bench.json
+timeout -k 10 200 python3 $CMD --no-cpu > $OUT/bench_2.json 2> $OUT/bench_2.err || { tail $OUT/bench_2.err; exit 1; }
+DSX_BENCH_STAMPS=0 timeout -k 10 200 python3 $CMD --no-cpu > $OUT/bench_nostamps.json 2> $OUT/bench_nostamps.err || { tail $OUT/bench_nostamps.err; exit 1; }
+echo "again: $(cat $OUT/bench_2.json)"; echo "no stamps: $(cat $OUT/bench_nostamps.json)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $CMD > $OUT/trace_bench.json 2> $OUT/trace.err || { tail $OUT/trace.err; exit 1; }
+cat $OUT/trace_bench.json
+timeout -s KILL 180 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d $OUT/pmc_rdreq -o run --output-format csv -- python3 $CMD --no-cpu > $OUT/pmc_rdreq.json 2> $OUT/pmc_rdreq.err || { tail $OUT/pmc_rdreq.err; exit 1; }
+python3 tools/traffic_json.py $OUT/pmc_rdreq 8589934592 uniform > $OUT/traffic_uniform_8589934592.json && cat $OUT/traffic_uniform_8589934592.json
+timeout -s KILL 180 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -d $OUT/pmc_clk -o run --output-format csv -- python3 $CMD --no-cpu > $OUT/pmc_clk.json 2> $OUT/pmc_clk.err || { tail $OUT/pmc_clk.err; exit 1; }
+for w in dedup zeros; do
+  timeout -k 10 300 python3 $CMD --workload $w --no-cpu > $OUT/bench_$w.json 2> $OUT/bench_$w.err || { tail $OUT/bench_$w.err; exit 1; }
+  echo "$w: $(cat $OUT/bench_$w.json)"
+done
+timeout -k 10 400 python3 tools/digest_rate.py 1 4 16 > $OUT/digest_rate.json 2> $OUT/digest_rate.err || { tail $OUT/digest_rate.err; exit 1; }
+timeout -k 10 600 python3 tools/make_rate.py 1 4 > $OUT/make_rate.json 2> $OUT/make_rate.err || { tail $OUT/make_rate.err; exit 1; }
+python3 -c "
+import json
+for r in json.load(open('$OUT/digest_rate.json'))['rows']: print('ids', r['gib'], {k: v for k, v in r.items() if k.endswith('_gibs')})
+for r in json.load(open('$OUT/make_rate.json'))['rows']: print('make', r['gib'], {k: v for k, v in r.items() if k.endswith('gibs')})"
+echo done
