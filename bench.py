@@ -62,6 +62,10 @@ def parse():
                          "uniform blob per GPU (256 GiB over 8 GPUs)")
     ap.add_argument("--config2", action="store_true",
                     help="BASELINE config 2's shape: 1 GiB of the seed-1 uniform blob per GPU")
+    ap.add_argument("--avg", type=int, default=64,
+                    help="average chunk size in KiB, min = avg/4, max = 4*avg (SURVEY.md 8(d)'s "
+                         "sweep 16/64/256, chunker_test.go:191's set); default 64 = desync make's "
+                         "16/64/256 KiB")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the cpu_baseline leg (0: the job's CPU share)")
@@ -85,6 +89,8 @@ def parse():
                    else "config 2" if (args.workload, args.gib, args.seed) == ("uniform", 1.0, 1)
                    else "config 3" if (args.workload, args.gib) == ("dedup", 16.0)
                    else "config 4" if (args.workload, args.gib) == ("zeros", 64.0) else None)
+    if args.avg != 64:
+        args.config = None
     if args.inflight <= 0:
         args.inflight = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
     return args
@@ -204,6 +210,9 @@ def cpu_baseline(host_blob, threads=None):
 
 def main():
     args = parse()
+    global MIN, AVG, MAX
+    AVG = args.avg * 1024
+    MIN, MAX = AVG // 4, AVG * 4
     import torch
     from desync_amd import _lib
     import desync_amd
@@ -369,7 +378,7 @@ def main():
             "config": {
                 "workload": (f"{args.gib:g} GiB {args.workload} blob per GPU"
                              f"{' (BASELINE ' + args.config + ' shape)' if args.config else ''}, "
-                             f"desync make min/avg/max 16/64/256 KiB, device-resident blob -> "
+                             f"desync make min/avg/max {MIN >> 10}/{AVG >> 10}/{MAX >> 10} KiB, device-resident blob -> "
                              f"cut list in HBM"),
                 "bytes_per_gpu": n,
                 "chunks": int(chunks),

@@ -140,6 +140,33 @@ def test_uniform_9gib_two_pieces(dctx, monkeypatch, params, tail):
     assert got[-1] == n and np.any(got > (1 << 32)) and np.any((got > 8 * GiB) & (got < 9 * GiB))
 
 
+@pytest.mark.parametrize("n,params", [(int(3.25 * GiB) + 4567, (MIN, AVG, MAX)),
+                                      (4 * GiB - 999, (4096, 16384, 65536))])
+def test_two_region_sizes_edges(dctx, n, params):
+    """One piece just above the two-region-size threshold (three big regions
+    per wave slot, ~3.1 GiB on 256 CUs) and one with a partial last tail
+    region, with a 3 MiB zero run where the big regions give way to the tail
+    regions (~1.03 GiB before the end) and a repeated 1 MiB block inside the
+    tail: cut for cut against the oracle (two region sizes)."""
+    import torch
+    import desync_amd
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _gen(dctx, t, 0, n, "uniform", 11)
+    z0 = n - int(1.1 * GiB)
+    t[z0:z0 + 3 * MiB].zero_()
+    t[n - 5 * MiB:n - 4 * MiB].copy_(t[n - 9 * MiB:n - 8 * MiB])
+    host = t.cpu().numpy()
+    got = desync_amd.cut_device(t.data_ptr(), n, *params, ctx=dctx)
+    del t
+    _free()
+    ref = o.chunk_parallel(host, *params, o.default_threads())
+    assert got.size == ref.size and np.array_equal(got, ref)
+    if params == (MIN, AVG, MAX):
+        # the zero run holds only forced max-size cuts
+        inside = got[(got > z0 + MAX) & (got < z0 + 3 * MiB)]
+        assert inside.size and np.all(np.diff(inside) == MAX)
+
+
 def test_config5_8x32gib_shards(dctx):
     """256 GiB range-sharded over 8 ranks (one process, one context per rank,
     seam records exchanged by hand as the all-gather would)."""
