@@ -187,6 +187,34 @@ class Chunker:
         v = self._win[s - self._wbase:e - self._wbase]
         return s, (v if self._zero_copy else v.tobytes())
 
+    def _next_run(self):
+        """What Next() would return over its next calls, up to the next point
+        where it reads (the reference's fillBuffer check, or the read-ahead):
+        a list of (start, bytes copy, ID or None), [] at the end of the
+        stream.  The first chunk comes from Next() itself, so reader errors
+        surface exactly where Next() raises them.  (ChunkStream: one call per
+        run instead of one per chunk.)"""
+        s, b = self.Next()
+        if not b:
+            return []
+        out = [(s, b if not self._zero_copy else b.tobytes(), self._last_id)]
+        q, qi, n = self._q, self._qi, len(self._q)
+        if qi >= n or self._win is None:
+            return out
+        mx, R, ra, pos = self.params.max, self._R, self._ra, self._pos
+        win, wb, ids = self._win, self._wbase, self._qids if self._idbuf is not None else None
+        cur = self._cur
+        while qi < n and R - cur >= mx and not (ra and pos - cur < ra // 2):
+            e = q[qi]
+            out.append((cur, win[cur - wb:e - wb].tobytes(),
+                        ids[32 * qi:32 * qi + 32] if ids is not None else None))
+            cur = e
+            qi += 1
+        self._qi, self._cur = qi, cur
+        if ids is not None:
+            self._last_id = out[-1][2]
+        return out
+
     def EnableIDs(self, algo=None):
         """Compute every chunk's Digest.Sum on the GPU next to its cut (for
         ChunkStream); only before the first Next().  ``algo``: "sha512-256"

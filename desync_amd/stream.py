@@ -121,22 +121,31 @@ def ChunkStream(ctx, c, ws, n):
     for t in threads:
         t.start()
     group = []
+    done = getattr(ctx, "done", None) if ctx is not None else None
+    run_of = getattr(c, "_next_run", None)  # (Next() for a run of chunks; this package's Chunker)
     try:
         while not errors:
-            if ctx is not None and getattr(ctx, "done", lambda: False)():
+            if run_of is not None:
+                run = run_of()
+            else:
+                start, b = c.Next()
+                run = [(start, bytes(b), c.ChunkID())] if b else []
+            if not run:
                 break
-            start, b = c.Next()
-            if not b:
+            stop = False
+            for start, data, cid in run:  # data: a clone (slices.Clone, index.go:196-200)
+                if done is not None and done():
+                    stop = True
+                    break
+                if cid is None:
+                    raise RuntimeError("chunker produced a chunk without a GPU chunk ID")
+                chunks.append(IndexChunk(cid, start, len(data)))
+                group.append(Chunk(cid, data))
+                if len(group) >= _BATCH:
+                    work.put(group)
+                    group = []
+            if stop:
                 break
-            cid = c.ChunkID()
-            if cid is None:
-                raise RuntimeError("chunker produced a chunk without a GPU chunk ID")
-            data = bytes(b)  # slices.Clone (index.go:196-200)
-            chunks.append(IndexChunk(cid, start, len(data)))
-            group.append(Chunk(cid, data))
-            if len(group) >= _BATCH:
-                work.put(group)
-                group = []
     finally:
         if group and not errors:
             work.put(group)

@@ -380,6 +380,37 @@ def test_chunk_stream_large(algo):
     assert idx.Index.FeatureFlags == o.CA_FORMAT_EXCLUDE_NO_DUMP | o.CA_FORMAT_SHA512256
 
 
+def test_chunker_runs_equal_next():
+    """Chunker._next_run (ChunkStream's path: the chunks Next() would return up
+    to its next read, in one call) gives Next()'s (start, bytes, ID) sequence,
+    with IDs on and off, across 8 MiB reads and a 10*max refill boundary."""
+    import desync_amd
+    data = np.concatenate([o.synth_uniform(48, 0, 40 << 20), np.zeros(2 << 20, np.uint8),
+                           o.synth_uniform(49, 0, (9 << 20) + 3)]).tobytes()
+    for ids in (False, True):
+        a = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX)
+        b = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX)
+        if ids:
+            a.EnableIDs()
+            b.EnableIDs()
+        want = []
+        while True:
+            s, chunk = a.Next()
+            if not chunk:
+                break
+            want.append((s, bytes(chunk), a.ChunkID()))
+        got, runs = [], 0
+        while True:
+            run = b._next_run()
+            if not run:
+                break
+            runs += 1
+            got.extend(run)
+        a.close()
+        b.close()
+        assert got == want and runs < len(want)
+
+
 def test_chunk_stream_errors():
     """A failing store raises out of ChunkStream; a cancelled ctx stops the
     producer and returns the chunks so far (index.go:203-206)."""
