@@ -52,6 +52,22 @@ def main():
 
     st_cs, idx = repeat(lambda: desync_amd.ChunkStream(
         None, desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX), NullStore(), 4), n)
+    class PerChunk:  # the same Chunker without _next_run: ChunkStream's Next()-per-chunk path
+        def __init__(self, c):
+            object.__setattr__(self, "_c", c)
+
+        def __getattr__(self, k):
+            if k == "_next_run":
+                raise AttributeError(k)
+            return getattr(self._c, k)
+
+        def __setattr__(self, k, v):
+            setattr(self._c, k, v)
+
+    st_pc, idx_pc = repeat(lambda: desync_amd.ChunkStream(
+        None, PerChunk(desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX)), NullStore(), 4), n)
+    assert [(c.Start, c.Size, c.ID) for c in idx_pc.Chunks] == \
+        [(c.Start, c.Size, c.ID) for c in idx.Chunks]
     got = np.array([c.Start + c.Size for c in idx.Chunks], dtype=np.uint64)
     assert np.array_equal(got, want), "ChunkStream cut list differs"
     import hashlib
@@ -61,10 +77,13 @@ def main():
                       "gibs": st_zc["gibs_median"], "next_zero_copy": st_zc,
                       "next_copy_gibs": st_copy["gibs_median"], "next_copy": st_copy,
                       "chunkstream_gibs": st_cs["gibs_median"], "chunkstream": st_cs,
+                      "chunkstream_per_chunk_gibs": st_pc["gibs_median"],
+                      "chunkstream_per_chunk": st_pc,
                       "note": "io.BytesIO reader (readinto into the library's pinned buffer); "
                               "Next with zero_copy views (Go's aliasing rule) and with the "
-                              "default bytes copy; ChunkStream = Next + GPU SHA-512/256 IDs + "
-                              "bytes clone + store call per chunk; medians of DSX_RATE_REPS "
+                              "default bytes copy; ChunkStream = runs of chunks (Chunker._next_run) + GPU SHA-512/256 "
+                              "IDs + bytes clone + store call per chunk; chunkstream_per_chunk = "
+                              "the same through one Next() per chunk; medians of DSX_RATE_REPS "
                               "(10) runs with min/max"}))
 
 
