@@ -975,6 +975,7 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
     if (nseg <= 1024) hipLaunchKernelGGL(fixup_fast_kernel<1>, dim3(1), dim3(1024), 0, c->stream, ta);
     else if (nseg <= 2048) hipLaunchKernelGGL(fixup_fast_kernel<2>, dim3(1), dim3(1024), 0, c->stream, ta);
     else if (nseg <= 4096) hipLaunchKernelGGL(fixup_fast_kernel<4>, dim3(1), dim3(1024), 0, c->stream, ta);
+    else if (nseg <= 5120) hipLaunchKernelGGL(fixup_fast_kernel<5>, dim3(1), dim3(1024), 0, c->stream, ta);
     else if (nseg <= 8192) hipLaunchKernelGGL(fixup_fast_kernel<8>, dim3(1), dim3(1024), 0, c->stream, ta);
     else hipLaunchKernelGGL(fixup_fast_kernel<9>, dim3(1), dim3(1024), 0, c->stream, ta);
   } else {

@@ -58,18 +58,17 @@ struct WaveLdsSrc {
       load();
     }
   }
+  // (lanes past n hold 0xFFFFFFFF, which is also "none": the first lane
+  // above ar32 needs no range check, and a window with no such lane is full)
   __device__ uint32_t next_after32(uint32_t ar32) {
-    while (true) {
-      const uint64_t m = __ballot(v > ar32);
-      if (m) {
-        const uint32_t f = (uint32_t)__builtin_ctzll(m);
-        if (base + f >= n) return 0xFFFFFFFFu;
-        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)f);
-      }
+    uint64_t m = __ballot(v > ar32);
+    while (__builtin_expect(m == 0, 0)) {
       if (base + 64u >= n) return 0xFFFFFFFFu;
       base += 64u;
       load();
+      m = __ballot(v > ar32);
     }
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(m));
   }
   __device__ uint64_t first_in(uint64_t a, uint64_t b) {
     const uint32_t r = next_after(a - lo);  // a >= lo always (a = s+min, s >= lo)
@@ -132,17 +131,21 @@ __device__ __forceinline__ RelChain rel_chain(const ChainParams& w, uint64_t lo)
   r.end_at = r.is_last ? r.L : 0xFFFFFFFFu;
   return r;
 }
-// next(s) of chunker.go:206-277 for a relative chain position s (< L when
-// is_last); kRelUndet if the successor depends on bytes beyond the piece.
-// Straight-line scalar code around one ballot step (the walks are
-// latency-bound: every branch and wait is on the chain's critical path).
-__device__ __forceinline__ uint32_t rel_next(uint32_t s, WaveLdsSrc& src, const RelChain& w) {
-  if (s >= w.tail_at) return w.L;                  // chunker.go:215-217
+// next(s) of chunker.go:206-277 for a relative chain position s < tail_at
+// (the walks test s >= tail_at, which is <= end_at, once per step and sort
+// out the chain's end on that rare branch: next = L, chunker.go:215-217);
+// kRelUndet if the successor depends on bytes beyond the piece.  kRelUndet is
+// above every relative position, so the walks test only nx > er on the way
+// out: two scalar compares a step fewer (the steps are bound by the CU's one
+// scalar unit).
+__device__ __forceinline__ uint32_t rel_step(uint32_t s, WaveLdsSrc& src, const RelChain& w) {
   const uint32_t lim = min(s + w.max, w.lim_cap);  // chunker.go:221
   const uint32_t c = src.next_after32(s + w.min);  // chunker.go:259-271
   if (c <= lim) return c;                          // (none = 0xFFFFFFFF > lim)
   return lim > w.undet_at ? kRelUndet : lim;       // chunker.go:276
 }
+static_assert(kRelUndet > kRelClamp, "kRelUndet must exceed every relative position");
+
 
 
 __device__ __forceinline__ uint64_t seg_start(const StitchArgs& a, uint64_t s0, uint32_t k) {

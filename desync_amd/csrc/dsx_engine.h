@@ -29,7 +29,7 @@ template <int NT>
 __global__ void walk_kernel(StitchArgs a);
 __global__ void fixup_kernel(StitchArgs a);
 template <int PER>
-__global__ void fixup_fast_kernel(StitchArgs a);  // PER = 1, 2, 4, 8, 9
+__global__ void fixup_fast_kernel(StitchArgs a);  // PER = 1, 2, 4, 5, 8, 9
 template <int PER>
 __global__ void finish_kernel(StitchArgs a);
 __global__ void gather_kernel(StitchArgs a);

@@ -243,7 +243,10 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
   // A chain step is a ballot over the 64 candidates the wave holds in a
   // register, s_ff1 and a readlane; the chain's cuts go into one register
   // (lane i = cut i) and to LDS once at the end, so no step
-  // waits on LDS (each step's LDS store used to cost an lgkmcnt(0) wait)
+  // waits on LDS (each step's LDS store used to cost an lgkmcnt(0) wait).
+  // (One lane per chain, a cursor into the LDS candidates, was slower: 37.1
+  // against 31.4 us per 8 GiB piece, its steps wait on dependent LDS reads;
+  // profiles/r04r.)
   if (!dense) {
     for (uint32_t t = wv; t < nwalk; t += kWaves) {
       const uint32_t k = kFirst + t;
@@ -257,10 +260,17 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
       uint32_t ns = 0, why = 0;
       uint32_t specv = 0;  // lane i: the chain's i-th cut (i < 64)
       while (true) {
-        if (x >= rc.end_at) { why = 1; break; }
-        const uint32_t nx = rel_next(x, src, rc);
-        if (nx == kRelUndet) { why = 2; break; }
-        if (nx > er) break;
+        uint32_t nx;
+        if (__builtin_expect(x >= rc.tail_at, 0)) {  // (tail_at <= end_at)
+          if (x >= rc.end_at) { why = 1; break; }
+          nx = rc.L;                                   // chunker.go:215-217
+        } else {
+          nx = rel_step(x, src, rc);
+        }
+        if (__builtin_expect(nx > er, 0)) {  // (kRelUndet > er)
+          if (nx == kRelUndet) why = 2;
+          break;
+        }
         specv = ln == ns ? nx : specv;  // (v_cmp + v_cndmask; no lane >= 64)
         ++ns;
         last = nx;
@@ -316,10 +326,17 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
     const bool have_spec = sn != 0xFFFFFFFFu;
     const uint32_t specv = have_spec && ln < sn ? s_spec[t * a.scap + ln] : 0xFFFFFFFFu;
     while (true) {
-      if (x >= rc.end_at) { flags |= kSegEnd; break; }
-      const uint32_t nx = rel_next(x, src, rc);
-      if (nx == kRelUndet) { flags |= kSegUndet; break; }
-      if (nx > er) break;
+      uint32_t nx;
+      if (__builtin_expect(x >= rc.tail_at, 0)) {  // (tail_at <= end_at)
+        if (x >= rc.end_at) { flags |= kSegEnd; break; }
+        nx = rc.L;                                   // chunker.go:215-217
+      } else {
+        nx = rel_step(x, src, rc);
+      }
+      if (__builtin_expect(nx > er, 0)) {  // (kRelUndet > er)
+        if (nx == kRelUndet) flags |= kSegUndet;
+        break;
+      }
       if (nx > sr) {
         if (ln == (n & 63u) && n < a.scap) out[n] = lo + nx;  // spread the stores over lanes
         ++n;
@@ -694,6 +711,8 @@ __global__ __launch_bounds__(kFixThreads) void fixup_fast_kernel(StitchArgs a) {
 template __global__ void fixup_fast_kernel<1>(StitchArgs);
 template __global__ void fixup_fast_kernel<2>(StitchArgs);
 template __global__ void fixup_fast_kernel<4>(StitchArgs);
+// (an 8 GiB piece after the first in 2 MiB segments: 4097 of them)
+template __global__ void fixup_fast_kernel<5>(StitchArgs);
 template __global__ void fixup_fast_kernel<8>(StitchArgs);
 // (an 8 GiB piece after the first: its stitch anchors max bytes before the
 // piece, so 8193 one-MiB segments)

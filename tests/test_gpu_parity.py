@@ -563,13 +563,16 @@ def test_chunk_ids_both_kernels(monkeypatch, pc, algo):
         ctx.close()
 
 
+@pytest.mark.parametrize("nch", [220_000, 60_000])
 @pytest.mark.parametrize("lpt", ["1", "0"])
 @pytest.mark.parametrize("algo", ["sha512-256", "sha256"])
-def test_chunk_ids_longest_first(monkeypatch, lpt, algo):
-    """More chunks than digest_kernel has lanes (~200 K, sizes 0 .. 1000 B
-    with a few of 100 KiB and empty ones): the queue hands them out longest
-    first (DSX_DIGEST_LPT=1, the default: a counting sort by size class) or in
-    index order (0); every ID lands at its chunk's index either way."""
+def test_chunk_ids_longest_first(monkeypatch, lpt, algo, nch):
+    """~200 K chunks (more than digest_kernel's SHA-512 lanes, fewer than its
+    SHA-256 lanes) and ~60 K (fewer than either: one chunk per lane), sizes
+    0 .. 1000 B with a few of 100 KiB and empty ones: the chunks go out
+    longest first (DSX_DIGEST_LPT=1, the default: a counting sort by size
+    class) or in index order (0); every ID lands at its chunk's index either
+    way."""
     import hashlib
     import desync_amd
     from desync_amd import _lib
@@ -581,11 +584,11 @@ def test_chunk_ids_longest_first(monkeypatch, lpt, algo):
         total = (100 << 20) + 3
         arr = rng.integers(0, 256, size=total, dtype=np.uint8)
         t = torch_dev(arr)
-        sizes = rng.integers(0, 1000, size=220_000)
+        sizes = rng.integers(0, 1000, size=nch)
         sizes[rng.integers(0, sizes.size, 60)] = 100 << 10
         ends = np.cumsum(sizes).astype(np.uint64)
         ends = ends[ends <= total]
-        assert ends.size > 150_000
+        assert ends.size > 0.7 * nch
         code = _lib.DSX_DIGEST_SHA512_256 if algo == "sha512-256" else _lib.DSX_DIGEST_SHA256
         name = "sha512_256" if algo == "sha512-256" else "sha256"
         got = desync_amd.chunk_ids(t.data_ptr(), total, ends, 0, ctx=ctx, algo=code)
