@@ -167,6 +167,26 @@ def test_two_region_sizes_edges(dctx, n, params):
         assert inside.size and np.all(np.diff(inside) == MAX)
 
 
+@pytest.mark.parametrize("n", [4 * GiB + 3 * MiB + 123, 6 * GiB + 7])
+def test_stitch_segment_doubling(dctx, n):
+    """Pieces whose 1 MiB stitch segments would number more than 4097 get 2 MiB
+    ones (dsx_api.cpp stitch_seg): 4 GiB + 3 MiB is 2050 of them (just past
+    finish_kernel's 2048: fixup_fast_kernel<4> + gather), 6 GiB 3072; cut for
+    cut against the oracle, with a zero run across a 2 MiB segment boundary."""
+    import torch
+    import desync_amd
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _gen(dctx, t, 0, n, "uniform", 19)
+    z0 = 3 * GiB + 2 * MiB - 300 * 1024  # (a 2 MiB boundary inside the run)
+    t[z0:z0 + MiB].zero_()
+    host = t.cpu().numpy()
+    got = desync_amd.cut_device(t.data_ptr(), n, MIN, AVG, MAX, ctx=dctx)
+    del t
+    _free()
+    ref = o.chunk_parallel(host, MIN, AVG, MAX, o.default_threads())
+    assert got.size == ref.size and np.array_equal(got, ref)
+
+
 def test_config5_8x32gib_shards(dctx):
     """256 GiB range-sharded over 8 ranks (one process, one context per rank,
     seam records exchanged by hand as the all-gather would)."""
