@@ -517,14 +517,16 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   batches = line ? S / (3 * kLine) : (S / kRound + 1) / (uint32_t)cfgBR;
   const uint64_t region_bytes = 64ull * S;
   uint64_t nregions = len == 0 ? 0 : (span + region_bytes - 1) / region_bytes;
-  // Two region sizes (DSX_TAIL_SPLIT = k > 1, default 3; line scan, pieces of
+  // Two region sizes (DSX_TAIL_SPLIT = k > 1, default 4; line scan, pieces of
   // at least three big regions per wave slot): the last ~one big region's
   // worth of bytes per wave slot is cut into regions with k times shorter lane
   // segments, so the waves that drain the work queue last hold small regions
   // (DSX_TAIL_MULT = j: j big regions' worth per wave slot).  On the 8 GiB
   // pieces the waves end together (wave_busy 0.947 -> 0.98) and the scan is
-  // 1 % faster; k = 4 the same with more warm-up lines (HBM reads 1.021 x the
-  // input against 1.014), k = 2, 8 and j = 2 less (profiles/r04d, r04e, r04g)
+  // 1 % faster; k = 2, 6, 8 and j = 2 less (profiles/r04d, r04e, r04g, r04aa).
+  // (k = 3 was the default while every lane read a warm-up line: k = 4 read
+  // 1.021 x the input against 1.018; since the warm-up handoff only lane 0 of
+  // a region does, and k = 4 is 0.4-0.5 % ahead, profiles/r04ab.)
   uint64_t nbig = nregions, S2 = 0;
   if (line && !cc.dense && !cc.behind && c->tail_split > 1 && len > 0) {
     const uint64_t m = S / (3 * kLine), m2 = std::max<uint64_t>(1, m / (uint64_t)c->tail_split);

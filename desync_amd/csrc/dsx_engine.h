@@ -128,7 +128,7 @@ struct dsx_ctx {
   int digest_pc_chunks = 2;           // DSX_DIGEST_PC_CHUNKS: auto uses it up to this many chunks per grid lane
   int scanl_waves = 8;                // waves per workgroup of scanl_kernel
   uint32_t lane_target = 8448;        // DSX_LANE_TARGET: longest line-scan lane segment
-  int tail_split = 3;                 // DSX_TAIL_SPLIT=k: tail regions with k x shorter lane segments (0/1: one size)
+  int tail_split = 4;                 // DSX_TAIL_SPLIT=k: tail regions with k x shorter lane segments (0/1: one size)
   int tail_mult = 1;                  // DSX_TAIL_MULT=j: the split tail is j big regions per wave slot
   uint64_t seg_max_mult = 4;          // DSX_SEG_MAX: stitch segment = max(mult * max, floor)
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR

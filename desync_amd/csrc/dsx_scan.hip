@@ -658,7 +658,11 @@ DSX_SCAN_INST_ALL(2, 1, 16, 4, false)
 // fetched twice from HBM (TCC_EA0_RDREQ_128B = 1.18 x the input bytes,
 // tools/pmc_tcc.sh): the L2 dropped a half-used line before the row next to
 // it arrived.  The warm-up is the last 48 bytes of the line before the
-// segment (128/S extra reads).  One LDS staging line per lane (8 KiB per
+// segment -- for lane 0 of a region only: lanes 1..63 hash their first 48
+// positions from a zero window and drop them, and the lane before tests them
+// at the end of its own segment from 48 bytes they leave in LDS (the
+// handoff; HBM reads 1.018 -> 1.0004 x the input, profiles/r04z, r04ab).
+// One LDS staging line per lane (8 KiB per
 // wave): a batch is copied to registers, then the next batch's DMA is issued
 // at once, so it lands while this one is hashed.  A batch of 128 B is three
 // ring phases apart from the next (128 = 2*48 + 32), so the steady-state loop
@@ -683,6 +687,13 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   static_assert(LDSB <= kScanLds, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDSB];
   __shared__ uint32_t s_prog[kBal ? W : 1];  // batches hashed per wave (SIMD partner balancing)
+  // warm-up handoff: each lane's first 48 segment bytes, which the lane before
+  // it hashes and tests at the end of its own segment (lanes 1..63 read no
+  // warm-up line: 128 B of HBM read per lane segment saved)
+  constexpr int kHandoff = 48;
+  static_assert(LDSB + (int)sizeof(uint32_t) * (W + 256) + W * kWave * kHandoff + 16 * W <= kScanLds,
+                "LDS budget with the handoff");
+  __shared__ __attribute__((aligned(16))) uint8_t s_hand[W * kWave * kHandoff];
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[256];  // the table, landed by LDS-DMA
   // trace: the wave's first instruction (before the table fill)
   const uint64_t t_entry = VARIANT == 5 ? __builtin_amdgcn_s_memtime()
@@ -789,7 +800,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     for (int i = 0; i < NI; ++i) {
       uint32_t ssum = (uint32_t)i * 8u * rS + sb;
       asm volatile("" : "+s"(ssum));
-      vo[i] = ok ? ((i & 1) ? d1 : d0) + ssum : 0xFFFFFFF0u;
+      // (a warm-up line, b = 0: row 0 only = instruction 0, DMA lanes 0-7)
+      vo[i] = ok && (b != 0u || (i == 0 && lane < 8u)) ? ((i & 1) ? d1 : d0) + ssum : 0xFFFFFFF0u;
     }
     switch (a.nt_loads) {
       case 1: dma16x8<1>(rsrc, vo, stage_lds); break;
@@ -809,6 +821,23 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       asm volatile("" : "+s"(ssum));
       vo[i] = (b < 3u * M + 1u) ? ((i & 1) ? dbase1 : dbase0) + ssum : 0xFFFFFFF0u;
     }
+    switch (a.nt_loads) {
+      case 1: dma16x8<1>(rsrc, vo, stage_lds); break;
+      case 2: dma16x8<2>(rsrc, vo, stage_lds); break;
+      case 3: dma16x8<3>(rsrc, vo, stage_lds); break;
+      default: dma16x8<0>(rsrc, vo, stage_lds); break;
+    }
+  };
+
+  // a region's warm-up line (batch 0) for row 0 only; the other lanes take
+  // their window from the lane before (the handoff).  Kept apart from issue(),
+  // which runs at every line of the trip loop.
+  auto issue_warm = [&](const u32x4& rsrc, uint32_t sh, bool ok) {
+    if constexpr (VARIANT == 4) return;
+    uint32_t vo[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) vo[i] = 0xFFFFFFF0u;
+    vo[0] = ok && lane < 8u ? dbase0 - sh : 0xFFFFFFF0u;
     switch (a.nt_loads) {
       case 1: dma16x8<1>(rsrc, vo, stage_lds); break;
       case 2: dma16x8<2>(rsrc, vo, stage_lds); break;
@@ -862,7 +891,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       }
     }
     desc_of(region, rsrc, sh);
-    issue(rsrc, sh, 0u);
+    issue_warm(rsrc, sh, true);
   }
   if (wave == 0) {
     if (live && VARIANT != 4)
@@ -1026,7 +1055,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
           // or a big one stolen from a slower XCD's counter after it)
           issue_in(nrsrc, nsh, 0u, true, nS, dbase_of(nS, 0u), dbase_of(nS, 1u));
         } else {
-          issue(nrsrc, nsh, next < a.nregions ? 0u : 3u * M + 1u);
+          issue_warm(nrsrc, nsh, next < a.nregions);
         }
       }
       if constexpr (VARIANT == 5) dma_issue += __builtin_amdgcn_s_memtime() - tw2;
@@ -1158,6 +1187,13 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       }
     };
     fetch(1u);
+    {  // this segment's first 48 bytes, for the lane before (the handoff)
+      uint8_t* const my_hand = s_hand + (wave * kWave + lane) * kHandoff;
+#pragma unroll
+      for (int c = 0; c < kHandoff / 16; ++c)
+        *reinterpret_cast<uint4*>(my_hand + 16 * c) =
+            make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+    }
     static_for<D>([&](auto gc) __attribute__((always_inline)) { issue_sub(gc); });
     for (uint32_t t = 0; t < M; ++t) {
       // the successor's ticket, drawn mid-region: waves that started
@@ -1192,6 +1228,31 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       });
     }
 
+    {
+      // the first 48 positions of the next lane's segment, whose window reaches
+      // back into this one (that lane hashed them from a zero window and drops
+      // them): 6 more subgroups from the bytes it left in LDS, with this
+      // segment's ring and hash, hits at offsets S + 1 .. S + 48.  (Lane 63's
+      // next segment is the next region's, whose lane 0 reads its warm-up line;
+      // its extension hits are dropped below.)
+      const uint8_t* nb = s_hand + (wave * kWave + (lane < 63u ? lane + 1u : lane)) * kHandoff;
+#pragma unroll
+      for (int c = 0; c < kHandoff / 16; ++c) {
+        const uint4 q = *reinterpret_cast<const uint4*>(nb + 16 * c);
+        w[4 * c] = q.x;
+        w[4 * c + 1] = q.y;
+        w[4 * c + 2] = q.z;
+        w[4 * c + 3] = q.w;
+      }
+      static_for<6>([&](auto gc) __attribute__((always_inline)) {
+        constexpr int g = decltype(gc)::value;
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (g == 0) issue_sub(std::integral_constant<int, 0>{});
+        if constexpr (g + 1 < 6) issue_sub(std::integral_constant<int, g + 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        compute_sub(gc, S);
+      });
+    }
     const uint64_t t_hash_end = a.trace ? __builtin_amdgcn_s_memtime() : 0;
     // ---- region end: compact the lanes' hits into one sorted region list ----
     // valid cut offsets o: piece-relative p = lane_p + o in [1, len] and
@@ -1200,9 +1261,13 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     int64_t lo = 1 - lane_p;
     const int64_t lo2 = (int64_t)a.min_pos - (int64_t)a.piece_abs - lane_p;
     lo = lo > lo2 ? lo : lo2;
+    // (the handoff: lanes 1..63 drop offsets 1..48, hashed from a zero window;
+    // the lane before reports them as S + 1 .. S + 48, lane 63 excepted)
+    const uint32_t ext = lane < 63u ? (uint32_t)kHandoff : 0u;
+    if (lane > 0u && lo < (int64_t)kHandoff + 1) lo = (int64_t)kHandoff + 1;
     const uint32_t o_min = lo <= 1 ? 1u : (lo > (int64_t)S ? S + 1u : (uint32_t)lo);
     const int64_t hi = (int64_t)a.len - lane_p;
-    const uint32_t o_max = hi <= 0 ? 0u : (hi >= (int64_t)S ? S : (uint32_t)hi);
+    const uint32_t o_max = hi <= 0 ? 0u : (hi >= (int64_t)(S + ext) ? S + ext : (uint32_t)hi);
     const uint32_t n = cnt < a.lane_slots + kHitRegs ? cnt : a.lane_slots + kHitRegs;
     const bool spilled = __ballot(cnt > (uint32_t)kHitRegs) != 0;
     auto for_each_hit = [&](auto&& f) {

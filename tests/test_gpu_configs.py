@@ -113,22 +113,22 @@ def test_config4_64gib_zeros(dctx):
                                          ((MIN, AVG, MAX), 4)])
 def test_uniform_9gib_two_pieces(dctx, monkeypatch, params, tail):
     """> 2^32 bytes and two 8 GiB pieces: the carried chain state, 64-bit
-    offsets and the second piece's region grid, cut for cut.  tail = 3
-    (DSX_TAIL_SPLIT, the default): the 8 GiB piece's last regions have 3x
+    offsets and the second piece's region grid, cut for cut.  tail = 4
+    (DSX_TAIL_SPLIT, the default): the 8 GiB piece's last regions have 4x
     shorter lane segments (two region sizes in the scan and the stitch);
-    tail = 4: 4x; tail = 0: one region size."""
+    tail = 3: 3x; tail = 0: one region size."""
     import torch
     import desync_amd
     from desync_amd import _lib
     ctx = dctx
-    if tail != 3:
+    if tail != 4:
         monkeypatch.setenv("DSX_TAIL_SPLIT", str(tail))
         ctx = _lib.Context(0)
     n = 9 * GiB + 12345
     t = torch.empty(n, dtype=torch.uint8, device="cuda")
     _gen(ctx, t, 0, n, "uniform", 7)
     host = t.cpu().numpy()
-    if params == (MIN, AVG, MAX) and tail == 3:
+    if params == (MIN, AVG, MAX) and tail == 4:
         _check_bytes(host, 0, "uniform", 7)
     got = desync_amd.cut_device(t.data_ptr(), n, *params, ctx=ctx)
     if ctx is not dctx:
