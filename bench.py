@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--check", action="store_true",
                     help="N>1: compare the concatenated per-rank cut lists with one "
                          "dsx_cut_device over the whole blob on rank 0 (small sizes)")
+    ap.add_argument("--marks", default=None,
+                    help="write {t0, t1, bytes} (unix time around the timed steps) to this "
+                         "file, for tools/smu_summary.py's energy window")
     args = ap.parse_args()
     if args.config2:
         args.workload, args.gib, args.seed = "uniform", args.gib or 1.0, args.seed or 1
@@ -326,6 +329,7 @@ def main():
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
+    wall0 = time.time()
     chunks = 0
     if world == 1:
         for s in range(args.steps):
@@ -338,6 +342,10 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    wall1 = time.time()
+    if args.marks:
+        with open(args.marks, "w") as f:
+            json.dump({"t0": wall0, "t1": wall1, "bytes": n * args.steps, "rank": rank}, f)
     stamps = ctx.stamps_end() if stamping else []
     if dist:
         tdev = "cuda" if backend == "nccl" else "cpu"

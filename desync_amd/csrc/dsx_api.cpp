@@ -743,11 +743,21 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__>), g, b, 0, ss, sa); \
   else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__>), g, b, 0, ss, sa); \
   else
+// (the piece's region geometry picks TWO, as for the exact kernel: a one-size
+// instantiation over a two-size region list reads past the piece)
+#define DSX_LV(K, V, ...)                                                                  \
+  do {                                                                                     \
+    if (sa.lane_bytes2) hipLaunchKernelGGL((K<2, V, __VA_ARGS__, false, true>), g, b, 0, ss, sa); \
+    else hipLaunchKernelGGL((K<2, V, __VA_ARGS__, false, false>), g, b, 0, ss, sa);      \
+  } while (0)
 #define DSX_ABLATEL(K, ...)                                                                \
-  if (c->variant == 1) hipLaunchKernelGGL((K<2, 1, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
-  else if (c->variant == 3) hipLaunchKernelGGL((K<2, 3, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
-  else if (c->variant == 4) hipLaunchKernelGGL((K<2, 4, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
-  else if (c->variant == 7 && mode == 2) hipLaunchKernelGGL((K<2, 7, __VA_ARGS__, false, false>), g, b, 0, ss, sa); \
+  if (c->variant == 1) DSX_LV(K, 1, __VA_ARGS__);                                        \
+  else if (c->variant == 3) DSX_LV(K, 3, __VA_ARGS__);                                   \
+  else if (c->variant == 4) DSX_LV(K, 4, __VA_ARGS__);                                   \
+  else if (c->variant == 7 && mode == 2) DSX_LV(K, 7, __VA_ARGS__);                      \
+  else if (c->variant == 8 && mode == 2) DSX_LV(K, 8, __VA_ARGS__);                      \
+  else if (c->variant == 9 && mode == 2) DSX_LV(K, 9, __VA_ARGS__);                      \
+  else if (c->variant == 10 && mode == 2) DSX_LV(K, 10, __VA_ARGS__);                    \
   else
 #else
 #define DSX_ABLATE(K, ...)
@@ -765,9 +775,8 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
   } while (0)
 #if DSX_DIAG
 #define DSX_TRACE_VARIANTS(WV, SUB, D)                                                    \
-  if (c->variant == 5) hipLaunchKernelGGL((scanl_kernel<2, 5, WV, SUB, D, false, false>), g, b, 0, ss, sa); \
-  else if (c->variant == 6 && mode == 2)                                                  \
-    hipLaunchKernelGGL((scanl_kernel<2, 6, WV, SUB, D, false, false>), g, b, 0, ss, sa);         \
+  if (c->variant == 5) DSX_LV(scanl_kernel, 5, WV, SUB, D);                               \
+  else if (c->variant == 6 && mode == 2) DSX_LV(scanl_kernel, 6, WV, SUB, D);             \
   else
 #else
 #define DSX_TRACE_VARIANTS(WV, SUB, D)
@@ -812,6 +821,9 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
 #undef DSX_LAUNCHL
 #undef DSX_ABLATE
 #undef DSX_ABLATEL
+#ifdef DSX_LV
+#undef DSX_LV
+#endif
 #undef DSX_TRACE_VARIANTS
     HIPCHK(c, hipGetLastError());
   }

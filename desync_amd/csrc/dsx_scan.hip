@@ -719,7 +719,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   // (VARIANT 7: 64 slots of 4 B per byte value instead of 32 of 8 B)
-  const uint32_t slot8 = VARIANT == 7 ? lane * 4u : (lane & 31u) * 8u;
+  const uint32_t slot8 = (VARIANT == 7 || VARIANT == 10) ? lane * 4u : (lane & 31u) * 8u;
   uint8_t* stage = lds + kTableBytes + wave * STG;
   // Waves w and w + W/2 share a SIMD (waves are placed on the SIMDs
   // cyclically).  VALU issue favours the older wave, so left alone the
@@ -907,7 +907,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     uint2 t;
     t.x = tv;
     t.y = __builtin_amdgcn_alignbit(tv, tv, 16);
-    if constexpr (VARIANT == 7) {
+    if constexpr (VARIANT == 7 || VARIANT == 10) {
 #pragma unroll
       for (int k = 0; k < (64 + TPV - 1) / TPV; ++k) {
         const uint32_t slot = (threadIdx.x >> 8) + (uint32_t)(k * TPV);
@@ -1080,7 +1080,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int k = (g % 16) * 8 + q;  // byte within the line
-        if constexpr (VARIANT == 7)
+        if constexpr (VARIANT == 7 || VARIANT == 10)
           L[g % NL][q] = *reinterpret_cast<const uint32_t*>(lds + lookup_addr(w[k >> 2], slot8, k & 3));
         else
           L[g % NL][q] = *reinterpret_cast<const uint64_t*>(lds + lookup_addr(w[k >> 2], slot8, k & 3));
@@ -1094,7 +1094,11 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         return;
       }
       lookups_landed<8>(L[g % NL]);
-      constexpr bool kTest = VARIANT == 0 || VARIANT == 4 || VARIANT == 5 || VARIANT == 7;
+      // (energy ablations, wrong results: 8 = no multiply (t = h), 9 = the 8 t
+      // values OR-ed with full-rate v_bitop3 instead of the v_min3 tree, 10 =
+      // 4-byte lookups, the ring takes T itself)
+      constexpr bool kTest = VARIANT == 0 || VARIANT == 4 || VARIANT == 5 || VARIANT == 7 ||
+                             VARIANT == 8 || VARIANT == 9 || VARIANT == 10;
       uint32_t t[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -1103,9 +1107,11 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
             VARIANT == 7 ? __builtin_amdgcn_alignbit(ring[rk], ring[rk], 16) : ring[rk];
         h = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(h, h, 31),
                                         (uint32_t)L[g % NL][q], outv, 0x96);
-        ring[rk] = VARIANT == 7 ? (uint32_t)L[g % NL][q] : (uint32_t)(L[g % NL][q] >> 32);
+        ring[rk] = (VARIANT == 7 || VARIANT == 10) ? (uint32_t)L[g % NL][q]
+                                                   : (uint32_t)(L[g % NL][q] >> 32);
         if constexpr (kTest) {
-          if constexpr (MODE == 2) t[q] = h * tcv.ninv;  // t + 1: one v_mul_lo_u32
+          if constexpr (VARIANT == 8) t[q] = h;
+          else if constexpr (MODE == 2) t[q] = h * tcv.ninv;  // t + 1: one v_mul_lo_u32
           else t[q] = is_cand<MODE>(h, tcv) ? 0u : 0xFFFFFFFFu;
         }
       }
@@ -1114,8 +1120,14 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       } else {
         const uint32_t thr = MODE == 2 ? tcv.vmax1 : 1u;
         uint32_t mn = t[0];
+        if constexpr (VARIANT == 9) {
+          mn = __builtin_amdgcn_bitop3_b32(t[0], t[1], t[2], 0xFE);  // a | b | c
+          const uint32_t m2 = __builtin_amdgcn_bitop3_b32(t[3], t[4], t[5], 0xFE);
+          mn = __builtin_amdgcn_bitop3_b32(mn, m2, t[6], 0xFE) | t[7];
+        } else {
 #pragma unroll
-        for (int q = 1; q < 8; ++q) mn = __builtin_elementwise_min(mn, t[q]);
+          for (int q = 1; q < 8; ++q) mn = __builtin_elementwise_min(mn, t[q]);
+        }
         if (__builtin_expect(__ballot(mn < thr) != 0, 0)) {
           uint32_t bits = 0;
           if (MODE == 2 && tcv.rot == 0) {
@@ -1366,6 +1378,19 @@ template __global__ void scanl_kernel<2, 4, 8, 8, 1, false, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 5, 8, 8, 1, false, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 6, 8, 8, 1, false, false>(ScanArgs);
 template __global__ void scanl_kernel<2, 7, 8, 8, 1, false, false>(ScanArgs);
+// (the same variants over a piece with two region sizes)
+template __global__ void scanl_kernel<2, 1, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 3, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 4, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 5, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 6, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 7, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 8, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 9, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 10, 8, 8, 1, false, true>(ScanArgs);
+template __global__ void scanl_kernel<2, 8, 8, 8, 1, false, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 9, 8, 8, 1, false, false>(ScanArgs);
+template __global__ void scanl_kernel<2, 10, 8, 8, 1, false, false>(ScanArgs);
 #endif
 DSX_SCANL_INST(8, 8, 1)  // D = 2 needs 16 more VGPRs than the 256 of two waves per SIMD
 
