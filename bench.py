@@ -211,6 +211,67 @@ def cpu_baseline(host_blob, threads=None):
     }
 
 
+def roofline_of(stamps, dt, workload):
+    """The roofline object of one rank from its scan launches' in-kernel
+    stamps (None without stamps)."""
+    if not stamps:
+        return None
+    dur = np.array([st.ms for st in stamps])
+    nb = np.array([st.bytes for st in stamps], dtype=np.float64)
+    cyc = sum(st.wave_cycles for st in stamps)
+    tick = sum(st.wave_ticks for st in stamps)
+    per_launch = int(np.median(nb))
+    achieved = float(nb.sum() / (dur.sum() / 1e3) / 1e9)
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": load_traffic(workload, per_launch),
+        "kernel": "dsx::scanl_kernel",
+        "bytes_per_launch": per_launch,
+        "launches": len(stamps),
+        "kernel_ms": round(float(dur.mean()), 4),
+        "kernel_ms_min_max": [round(float(dur.min()), 4), round(float(dur.max()), 4)],
+        "clock_mhz": round(100.0 * cyc / tick, 1) if tick else None,
+        "wave_busy": round(float(np.mean([st.busy for st in stamps])), 4),
+        "scan_share_of_step": round(float(dur.sum()) / (dt * 1e3), 4),
+        "timing": "in-kernel s_memrealtime stamps of the timed jobs' scan launches",
+    }
+
+
+def hbm_footprint(torch, blob, outs, ctxs):
+    """This rank's HBM: the blob, the cut-list buffers, and every library
+    context's pipeline buffers (dsx_stats_t.device_bytes), against the
+    device's capacity.  Raises if they would not fit (a config the GPU
+    cannot hold must fail here, not in a kernel)."""
+    free, total = torch.cuda.mem_get_info()
+    lib_bytes = [int(c.stats().device_bytes) for c in ctxs]
+    out_bytes = sum(o.numel() * o.element_size() for o in outs)
+    used = blob.numel() + out_bytes + sum(lib_bytes)
+    if used > total:
+        raise RuntimeError(f"HBM footprint {used} B exceeds the device's {total} B")
+    return {"blob_bytes": blob.numel(), "cut_list_bytes": out_bytes,
+            "context_bytes": lib_bytes, "total_bytes": used, "device_bytes": total,
+            "device_free_bytes": free, "frac_of_device": round(used / total, 4)}
+
+
+def dist_info(dist, backend, per_rank):
+    """What torch.distributed reports for the job: the backend of the
+    default group, its world size and, over RCCL, the library version."""
+    info = {"backend": dist.get_backend(), "requested": backend,
+            "world_size": dist.get_world_size(), "ranks_reporting": len(per_rank)}
+    if info["backend"] == "nccl":
+        try:
+            import torch
+            v = torch.cuda.nccl.version()
+            info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception as e:  # noqa: BLE001 -- reported, not fatal
+            info["rccl_version"] = f"unknown ({e})"
+    return info
+
+
 def main():
     args = parse()
     global MIN, AVG, MAX
@@ -323,9 +384,13 @@ def main():
             ln.run()
         run_lanes(args.warmup)
     torch.cuda.synchronize()
-    stamping = world == 1 and os.environ.get("DSX_BENCH_STAMPS", "1") != "0"  # (0: A/B of their cost)
-    if stamping:  # in-kernel stamps of exactly the timed jobs' scan launches
-        ctx.stamps_begin(args.steps * ((n + PIECE - 1) // PIECE) + 8)
+    stamping = os.environ.get("DSX_BENCH_STAMPS", "1") != "0"  # (0: A/B of their cost)
+    # in-kernel stamps of exactly the timed jobs' scan launches, on every
+    # library context of this rank (N > 1: one per pipeline lane)
+    stamp_ctxs = [ln.ctx for ln in lanes] if world > 1 else [ctx]
+    if stamping:
+        for c in stamp_ctxs:
+            c.stamps_begin(args.steps * ((n + PIECE - 1) // PIECE) + 8)
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
@@ -346,8 +411,13 @@ def main():
     if args.marks:
         with open(args.marks, "w") as f:
             json.dump({"t0": wall0, "t1": wall1, "bytes": n * args.steps, "rank": rank}, f)
-    stamps = ctx.stamps_end() if stamping else []
+    stamps = [st for c in stamp_ctxs for st in c.stamps_end()] if stamping else []
+    mine = {"rank": rank, "roofline": roofline_of(stamps, dt, args.workload), "hbm": hbm_footprint(
+        torch, blob, outs + ([sh.out for sh in lanes] if lanes else []), stamp_ctxs)}
+    per_rank = [mine]
     if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         tdev = "cuda" if backend == "nccl" else "cpu"
         tt = torch.tensor([dt], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -394,31 +464,26 @@ def main():
                 "jobs_in_flight": depth if world == 1 else len(lanes),
             },
         }
-        if world == 1 and stamps:
-            dur = np.array([st.ms for st in stamps])
-            nb = np.array([st.bytes for st in stamps], dtype=np.float64)
-            cyc = sum(st.wave_cycles for st in stamps)
-            tick = sum(st.wave_ticks for st in stamps)
-            per_launch = int(np.median(nb))
-            achieved = float(nb.sum() / (dur.sum() / 1e3) / 1e9)
-            traffic = load_traffic(args.workload, per_launch)
-            res["roofline"] = {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": "dsx::scanl_kernel",
-                "bytes_per_launch": per_launch,
-                "launches": len(stamps),
-                "kernel_ms": round(float(dur.mean()), 4),
-                "kernel_ms_min_max": [round(float(dur.min()), 4), round(float(dur.max()), 4)],
-                "clock_mhz": round(100.0 * cyc / tick, 1) if tick else None,
-                "wave_busy": round(float(np.mean([st.busy for st in stamps])), 4),
-                "scan_share_of_step": round(float(dur.sum()) / (dt * 1e3), 4),
-                "timing": "in-kernel s_memrealtime stamps of the timed jobs' scan launches",
-            }
+        rl = [r["roofline"] for r in per_rank]
+        if all(rl):
+            # N = 1: this rank's scan; N > 1: the slowest rank's (min frac),
+            # with every rank's own figures beside it
+            worst = min(rl, key=lambda x: x["frac"])
+            res["roofline"] = dict(worst)
+            if world > 1:
+                res["roofline"]["rank"] = rl.index(worst)
+                res["roofline"]["per_rank"] = [
+                    {k: x[k] for k in ("achieved", "frac", "kernel_ms", "clock_mhz", "launches")}
+                    for x in rl]
+                res["roofline"]["frac_min_max"] = [min(x["frac"] for x in rl),
+                                                   max(x["frac"] for x in rl)]
+        res["hbm"] = per_rank[0]["hbm"] if world == 1 else {
+            "per_rank_bytes": [r["hbm"]["total_bytes"] for r in per_rank],
+            "device_bytes": per_rank[0]["hbm"]["device_bytes"],
+            "max_frac": max(r["hbm"]["frac_of_device"] for r in per_rank),
+            "rank0": per_rank[0]["hbm"]}
+        if dist:
+            res["dist"] = dist_info(dist, backend, per_rank)
         if world == 1 and not args.no_cpu:
             # a bounded sample: the shard's first GiB (the leg is ~10-30 s of CPU work)
             host = blob[halo:halo + min(n, CPU_SAMPLE)].cpu().numpy()

@@ -81,6 +81,7 @@ class Stats(ctypes.Structure):
         ("repaired_segments", ctypes.c_uint64), ("dense_fallbacks", ctypes.c_uint64),
         ("scan_ms", ctypes.c_float), ("stitch_ms", ctypes.c_float),
         ("chunks_discarded", ctypes.c_uint64),
+        ("device_bytes", ctypes.c_uint64),
     ]
 
 

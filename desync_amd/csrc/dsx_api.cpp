@@ -168,14 +168,25 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   hipDeviceProp_t prop;
   CREATE_STEP(hipGetDeviceProperties(&prop, device));
   c->ncu = prop.multiProcessorCount;
+  // The product library reads only these DSX_* settings (INTEGRATION.md,
+  // "Environment"; each has a test).  Everything measured and rejected, and
+  // every diagnostic geometry, is read by libdsx_diag.so only.
+  if (const char* v = getenv("DSX_TAIL_SPLIT")) c->tail_split = std::max(0, std::min(8, atoi(v)));
+  if (const char* v = getenv("DSX_LANE_TARGET"))
+    c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
+  if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
+  if (const char* v = getenv("DSX_SCAN_NT")) c->scan_nt = atoi(v) & 3;
+  if (const char* v = getenv("DSX_DIGEST_PC")) c->digest_pc = atoi(v);
+  if (const char* v = getenv("DSX_DIGEST_LPT")) c->digest_lpt = atoi(v) != 0;
+  if (const char* v = getenv("DSX_INDEX_WINDOW")) c->index_window = (uint64_t)std::max(1L << 16, atol(v));
+  if (const char* v = getenv("DSX_INDEX_SLOT")) c->index_slot = (uint64_t)std::max(1L << 12, atol(v));
+  if (const char* v = getenv("DSX_INDEX_READERS")) c->index_readers = std::max(1, std::min(32, atoi(v)));
+#if DSX_DIAG
+  // ablation variants, alternative geometries and rejected experiments
   if (const char* m = getenv("DSX_TEST_MODE")) c->force_mode = atoi(m);
-#if DSX_DIAG  // ablation variants and alternative geometries: libdsx_diag.so only
   if (const char* v = getenv("DSX_SCAN_VARIANT")) c->variant = atoi(v);
   if (const char* v = getenv("DSX_SCAN_CFG")) c->scan_cfg = std::min(5, std::max(0, atoi(v)));
-#endif
-  if (const char* v = getenv("DSX_DIGEST_PC")) c->digest_pc = atoi(v);
   if (const char* v = getenv("DSX_DIGEST_PC_CHUNKS")) c->digest_pc_chunks = std::max(1, atoi(v));
-  if (const char* v = getenv("DSX_DIGEST_LPT")) c->digest_lpt = atoi(v) != 0;
   if (const char* v = getenv("DSX_PREFETCH")) c->prefetch_batches = std::max(0, atoi(v));
   if (const char* v = getenv("DSX_REGIONS_PER_SLOT")) c->regions_per_slot = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SCAN_LINE")) c->scan_line = atoi(v) != 0;
@@ -184,33 +195,27 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     c->trace_keep = atoi(v) == 2;  // keep the traces of the last 4 pieces (slot = seq % 4)
   }
   if (const char* v = getenv("DSX_WAVE_MAJOR")) c->wave_major = atoi(v) != 0;
-  if (const char* v = getenv("DSX_SCAN_NT")) c->scan_nt = atoi(v) & 3;
   if (const char* v = getenv("DSX_FIXUP_FAST")) c->fixup_fast = atoi(v) != 0;
   if (const char* v = getenv("DSX_FINISH")) c->finish = atoi(v) != 0;
-#if DSX_DIAG  // the stitch behind the scan (tasks inside later scans): libdsx_diag.so only
+  // the stitch behind the scan (tasks inside later scans)
   if (const char* v = getenv("DSX_FUSE")) c->fuse = atoi(v) != 0;
-#endif
-
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
-  if (const char* v = getenv("DSX_SEG_FLOOR")) c->seg_floor = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_SEG_TARGET")) c->seg_target = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_DIGEST_PF")) c->digest_pf = atoi(v) != 0;
-  if (const char* v = getenv("DSX_TAIL_SPLIT")) c->tail_split = std::max(0, std::min(8, atoi(v)));
   if (const char* v = getenv("DSX_TAIL_MULT")) c->tail_mult = std::max(1, std::min(4, atoi(v)));
-  if (const char* v = getenv("DSX_LANE_TARGET"))
-    c->lane_target = (uint32_t)std::max(384, std::min((int)kLineLaneMax, atoi(v)));
-  if (const char* v = getenv("DSX_INDEX_WINDOW")) c->index_window = (uint64_t)std::max(1L << 16, atol(v));
-  if (const char* v = getenv("DSX_INDEX_SLOT")) c->index_slot = (uint64_t)std::max(1L << 12, atol(v));
-  if (const char* v = getenv("DSX_INDEX_READERS")) c->index_readers = std::max(1, std::min(32, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
     const long lb = atol(v);
     if (lb >= 48 && lb % 48 == 0 && lb <= (long)kMaxLaneBytes) c->lane_bytes_override = (uint32_t)lb;
   }
+  // split streams: the scan on a high-priority (or CU-masked) stream, the
+  // stitch beside it on the CUs the scan leaves free
   if (const char* v = getenv("DSX_STITCH_CUS")) c->stitch_cus = std::max(0, std::min(c->ncu / 2, atoi(v)));
   if (const char* v = getenv("DSX_SCAN_MASK")) c->scan_mask = atoi(v) != 0;
+#endif
   CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   c->scan_stream = c->stream;
+#if DSX_DIAG
   if (c->stitch_cus > 0) {
     // The scan's grid leaves stitch_cus CUs free (one per XCD at 8), and its
     // stream has the highest priority, so the dispatcher places a scan's
@@ -236,6 +241,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
       CREATE_STEP(hipEventCreateWithFlags(&c->ev_stitch[i], hipEventDisableTiming));
     }
   }
+#endif
   CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
   // coherent: dsx_result polls the seq the GPU publishes here
   CREATE_STEP(hipHostMalloc((void**)&c->h_ring, kQueueDepth * sizeof(HostState), hipHostMallocCoherent));
@@ -352,9 +358,30 @@ extern "C" int dsx_copy(dsx_ctx_t* c, void* dst, const void* src, uint64_t n) {
   return DSX_OK;
 }
 
+// Every device buffer a context holds (all of them are DevBufs, dsx_engine.h;
+// tests/test_gpu_multiproc.py checks the sum against hipMemGetInfo).
+static uint64_t ctx_device_bytes(const dsx_ctx* c) {
+  uint64_t b = 0;
+  auto add = [&](const auto& d) { b += d.n * sizeof(*d.p); };
+  add(c->trace);
+  add(c->region_cnt), add(c->region_list), add(c->overflow), add(c->rep_cnt), add(c->rep_from);
+  add(c->flag_list), add(c->region_cnt2), add(c->region_list2), add(c->lane_slot);
+  add(c->seg_info), add(c->stage), add(c->rep), add(c->out_off), add(c->out);
+  add(c->dg_ends), add(c->dg_ids), add(c->dg_queue), add(c->dg_order), add(c->dg_cls);
+  add(c->state), add(c->seg_info2), add(c->stage2), add(c->spec), add(c->spec2);
+  for (int i = 0; i < dsx_ctx::Stream::kSlots; ++i)
+    add(c->st.dbuf[i]), add(c->st.dout[i]), add(c->st.dids[i]);
+  add(c->st.rng), add(c->st.dq);
+  for (const auto& k : c->sh.kept) add(k.cnt), add(k.list);
+  add(c->d_seam), add(c->d_all), add(c->zero_word), add(c->d_ext), add(c->d_info), add(c->d_emit);
+  add(c->stamp_ring), add(c->idx_win[0]), add(c->idx_win[1]), add(c->idx_snap);
+  return b;
+}
+
 extern "C" int dsx_get_stats(dsx_ctx_t* c, dsx_stats_t* out) {
   if (!c || !out) return DSX_E_INVAL;
   *out = c->stats;
+  out->device_bytes = ctx_device_bytes(c);
   return DSX_OK;
 }
 
@@ -813,8 +840,7 @@ int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_
           else DSX_LAUNCH(2, 2, 8, 8, false);
       }
 #else
-      if (c->prefetch_batches > 0) DSX_LAUNCH(2, 2, 8, 8, true);
-      else DSX_LAUNCH(2, 2, 8, 8, false);
+      DSX_LAUNCH(2, 2, 8, 8, false);
 #endif
     }
 #undef DSX_LAUNCH

@@ -634,8 +634,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scan_kernel(ScanArgs a) {
   template __global__ void scan_kernel<2, 3, BR, NBUF, W, SUB, PF>(ScanArgs); \
   template __global__ void scan_kernel<2, 4, BR, NBUF, W, SUB, PF>(ScanArgs);
 DSX_SCAN_INST(2, 2, 8, 8, false)
-DSX_SCAN_INST(2, 2, 8, 8, true)
 #if DSX_DIAG
+DSX_SCAN_INST(2, 2, 8, 8, true)  // DSX_PREFETCH (L2 prefetch: measured slower)
 DSX_SCAN_INST_DIAG(2, 2, 8, 8, false)
 DSX_SCAN_INST_DIAG(2, 2, 8, 8, true)
 #define DSX_SCAN_INST_ALL(BR, NBUF, W, SUB, PF) \

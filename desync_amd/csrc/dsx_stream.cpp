@@ -331,8 +331,10 @@ extern "C" int dsx_stream_begin(dsx_ctx_t* c, const dsx_params_t* p) {
   s.ids = -1;
   s.p = *p;
   s.batch = 8ull << 20;
+#if DSX_DIAG
   if (const char* v = getenv("DSX_STREAM_BATCH"))
     s.batch = std::max<uint64_t>(4096, (uint64_t)atoll(v));
+#endif
   s.hbase = s.hend = s.cur = s.skip = 0;
   s.next_slot = 0;
   s.last_chunk = nullptr;
@@ -535,8 +537,10 @@ extern "C" int dsx_stream_ids(dsx_ctx_t* c, int algo) {
     return DSX_E_STATE;
   }
   s.ids = algo;
-  if (algo >= 0 && !getenv("DSX_STREAM_BATCH"))
-    s.batch = std::max<uint64_t>(s.batch, 128ull << 20);  // digests are latency-bound: bigger batches
+#if DSX_DIAG
+  if (getenv("DSX_STREAM_BATCH")) return DSX_OK;
+#endif
+  if (algo >= 0) s.batch = std::max<uint64_t>(s.batch, 128ull << 20);  // digests are latency-bound: bigger batches
   return DSX_OK;
 }
 

@@ -407,6 +407,8 @@ typedef struct dsx_stats {
     uint64_t chunks_discarded;  /* cuts the stitch computed, then replaced by a repair: ChunksProduced
                                    = chunks + chunks_discarded (make.go:329-341 counts the workers'
                                    discarded overlap chunks too) */
+    uint64_t device_bytes;      /* HBM the context holds now (its pipeline buffers; filled in by
+                                   dsx_get_stats; the caller's blob and cut list are not counted) */
 } dsx_stats_t;
 int dsx_get_stats(dsx_ctx_t *ctx, dsx_stats_t *out);
 

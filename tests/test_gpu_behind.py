@@ -189,38 +189,79 @@ def scenario_timed_calls(fctx):
         assert 0 < st.scan_ms < 100 and st.stitch_ms == 0
 
 
+def _run_queued_jobs(ctx, ptr, n, njobs, depth, ref, stamps=False):
+    """bench.py's N = 1 step loop: njobs dsx_cut_device jobs over the same
+    device blob, DSX_NO_SYNC, up to `depth` in flight on one context, each
+    collected oldest first and compared in full with `ref`."""
+    import torch
+    import desync_amd
+    from desync_amd import _lib
+    p = desync_amd.Params(MIN, AVG, MAX)
+    L = _lib.lib()
+    cap = n // MIN + 4
+    outs = [torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(depth)]
+    cnt = ctypes.c_uint64()
+    pend = []
+    if stamps:
+        ctx.stamps_begin(njobs * ((n + (8 << 30) - 1) >> 33) + 8)
+
+    def collect():
+        i = pend.pop(0)
+        _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
+        assert cnt.value == ref.size
+        assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
+
+    for s in range(njobs):
+        if len(pend) == depth:
+            collect()
+        _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(ptr), n, ctypes.byref(p.c),
+                                    ctypes.c_void_p(outs[s % depth].data_ptr()), cap,
+                                    ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
+                   ctx.h)
+        pend.append(s % depth)
+    while pend:
+        collect()
+    return ctx.stamps_end() if stamps else []
+
+
 def scenario_bench_steady_state_counts(ctx):
     """bench.py's config-2 shape: 1 GiB uniform jobs queued 4 deep on one
     context give the same cut list as the oracle."""
     import torch
-    from desync_amd import _lib
     n = 1 << 30
     arr = o.synth_uniform(1, 0, n)
     ref = o.chunk_parallel(arr, MIN, AVG, MAX, 16)
     t = torch.from_numpy(arr).to("cuda")
     del arr
-    import desync_amd
-    p = desync_amd.Params(MIN, AVG, MAX)
-    L = _lib.lib()
-    outs = [torch.empty(n // MIN + 4, dtype=torch.int64, device="cuda") for _ in range(4)]
-    cnt = ctypes.c_uint64()
-    pend = []
-    for s in range(12):
-        if len(pend) == 4:
-            i = pend.pop(0)
-            _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
-            assert cnt.value == ref.size
-            assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
-        _lib.check(L.dsx_cut_device(ctx.h, ctypes.c_void_p(t.data_ptr()), n, ctypes.byref(p.c),
-                                    ctypes.c_void_p(outs[s % 4].data_ptr()), n // MIN + 4,
-                                    ctypes.byref(cnt), _lib.DSX_OUT_DEVICE | _lib.DSX_NO_SYNC),
-                   ctx.h)
-        pend.append(s % 4)
-    while pend:
-        i = pend.pop(0)
-        _lib.check(L.dsx_result(ctx.h, ctypes.byref(cnt)), ctx.h)
-        assert cnt.value == ref.size
-        assert np.array_equal(outs[i][:cnt.value].cpu().numpy().astype(np.uint64), ref)
+    _run_queued_jobs(ctx, t.data_ptr(), n, 12, 4, ref)
+
+
+def scenario_bench_headline_job(ctx):
+    """The job bench.py's default line is printed on (BASELINE config 5's
+    per-GPU shard): 32 GiB of dsx_gen_uniform seed 3 in HBM, four 8 GiB
+    pieces per job, 4 DSX_NO_SYNC jobs in flight on one context (so the
+    chain state is carried across 3 piece seams while later jobs queue
+    behind), in-kernel stamps on.  Every job's full cut list equals
+    oracle.chunk_parallel (make.go:69-127's split-and-align, C restatement)
+    over the oracle's own twin generator, and the count is the bench line's
+    config.chunks."""
+    import torch
+    from desync_amd import _lib
+    n = 32 << 30
+    host = o.synth_uniform_c(3, 0, n)
+    ref = o.chunk_parallel(host, MIN, AVG, MAX, o.default_threads())
+    assert ref.size == 524384 and int(ref[-1]) == n
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _lib.check(_lib.lib().dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 3), ctx.h)
+    # the device generator's bytes are the oracle's at the ends of each piece
+    for off in (0, (8 << 30) - (1 << 20), (16 << 30) - 4096, n - (1 << 20)):
+        m = min(1 << 20, n - off)
+        assert np.array_equal(t[off:off + m].cpu().numpy(), host[off:off + m]), off
+    del host
+    st = _run_queued_jobs(ctx, t.data_ptr(), n, 8, 4, ref, stamps=True)
+    assert len(st) == 8 * 4 and all(s.bytes == 8 << 30 for s in st)
+    assert all(0 < s.ms < 50 for s in st)
+    del t
 
 
 # ---- product library (no fused stitch) ----------------------------------------
@@ -243,6 +284,16 @@ def test_bench_steady_state_counts():
         scenario_bench_steady_state_counts(ctx)
     finally:
         ctx.close()
+
+
+def test_bench_headline_job():
+    ctx = _ctx()
+    try:
+        scenario_bench_headline_job(ctx)
+    finally:
+        ctx.close()
+    import torch
+    torch.cuda.empty_cache()
 
 
 def test_fuse_needs_the_diagnostic_build(monkeypatch):

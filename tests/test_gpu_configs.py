@@ -13,7 +13,8 @@ uniform blob, on the device, against the CPU oracle.
   every rank's list must equal the sequential chain, which is recomputed per
   rank on the device from the rank's true entry cut (the chain from any true
   cut c is the chunking of blob[c:], chunker.go:206-277) and checked against
-  the CPU oracle in a window at every seam.
+  the CPU oracle in a window at every seam; an interior rank and the last
+  rank are compared in full with the oracle over their whole range.
 
 Reference: make_test.go:16-80 (parallel == sequential at any size),
 chunker_test.go:69-131 (zeros -> max-size chunks).
@@ -241,3 +242,14 @@ def test_config5_8x32gib_shards(dctx):
         assert np.array_equal(mine[:ref.size], ref), r
     del buf
     _free()
+    # an interior rank and the last rank in full against the CPU oracle over
+    # their whole range [entry, hi + max): the chain from the true entry cut
+    for r in (3, world - 1):
+        lo, hi = r * span, (r + 1) * span
+        entry = int(lists[r - 1][-1])
+        wend = min(total, hi + MAX)
+        host = o.synth_uniform_c(3, entry, wend - entry)
+        ref = o.chunk_parallel(host, MIN, AVG, MAX, o.default_threads()) + np.uint64(entry)
+        del host
+        ref = ref[ref <= hi]
+        assert lists[r].size == ref.size and np.array_equal(lists[r], ref), r

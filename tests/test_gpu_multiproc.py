@@ -13,7 +13,9 @@ over "gloo" (RCCL needs one GPU per rank; the seam protocol is the same).
   one-GPU box can run: the asynchronous step with the all-gather and the
   agreement all-reduce on the library stream, pipelined over two lanes.
 """
+import ctypes
 import hashlib
+import json
 import os
 import socket
 import subprocess
@@ -117,7 +119,50 @@ def test_bench_two_ranks_gloo_check():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "check ok" in r.stderr, r.stderr[-2000:]
-    assert '"n_gpus": 2' in r.stdout
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    # the N > 1 line validates itself: what torch.distributed reports, every
+    # rank's in-kernel scan stamps, every rank's HBM footprint
+    assert line["dist"]["backend"] == "gloo" and line["dist"]["world_size"] == 2
+    assert line["dist"]["ranks_reporting"] == 2
+    rl = line["roofline"]
+    assert len(rl["per_rank"]) == 2 and all(x["launches"] >= 3 for x in rl["per_rank"])
+    assert rl["frac"] == min(x["frac"] for x in rl["per_rank"]) > 0
+    hbm = line["hbm"]
+    assert len(hbm["per_rank_bytes"]) == 2 and 0 < hbm["max_frac"] < 1
+    r0 = hbm["rank0"]
+    assert len(r0["context_bytes"]) == 3 and all(b > 0 for b in r0["context_bytes"])
+    assert r0["blob_bytes"] == int(0.25 * (1 << 30))
+
+
+def test_context_device_bytes_accounts_for_its_hbm():
+    """dsx_stats_t.device_bytes (bench.py's per-rank HBM footprint) covers
+    what the device lost to the context: hipMemGetInfo's drop across
+    creating a context and running a 1 GiB job, with the blob and the cut
+    list allocated before, is at least device_bytes and not much more (the
+    runtime's own stream / code-object memory)."""
+    import torch
+
+    import desync_amd
+    from desync_amd import _lib
+    n = 1 << 30
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    out = torch.empty(n // MIN + 4, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    ctx = _lib.Context(0)
+    try:
+        _lib.check(_lib.lib().dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 5), ctx.h)
+        got = desync_amd.cut_device(t.data_ptr(), n, MIN, AVG, MAX, ctx=ctx)
+        assert got.size > 0
+        torch.cuda.synchronize()
+        free1, _ = torch.cuda.mem_get_info()
+        dev = ctx.stats().device_bytes
+    finally:
+        ctx.close()
+    drop = free0 - free1
+    assert dev > (n // (8 * 1024))  # at least the region lists of a 1 GiB piece
+    assert dev <= drop <= dev + (256 << 20), (dev, drop)
 
 
 def _nccl_worker(port, q):
