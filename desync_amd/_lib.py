@@ -138,6 +138,24 @@ def _share_torch_hip_runtime():
         ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 
+# The DSX_* settings the product library reads (INTEGRATION.md,
+# "Environment"; tests/test_abi.py checks the library's strings against it).
+PRODUCT_ENV = ("DSX_TAIL_SPLIT", "DSX_LANE_TARGET", "DSX_SEG_FLOOR", "DSX_SCAN_NT",
+               "DSX_DIGEST_PC", "DSX_DIGEST_LPT", "DSX_INDEX_WINDOW", "DSX_INDEX_SLOT",
+               "DSX_INDEX_READERS")
+# Settings only libdsx_diag.so reads (scan ablations, other geometries,
+# rejected experiments), with the value the product library behaves as (None:
+# no such value).  Set to anything else with the product library they would
+# be silently ignored, so loading it refuses them.
+DIAG_ENV = {"DSX_SCAN_VARIANT": "0", "DSX_SCAN_CFG": "0", "DSX_FUSE": "0", "DSX_TEST_MODE": None,
+            "DSX_DIGEST_PC_CHUNKS": "2", "DSX_PREFETCH": "0", "DSX_REGIONS_PER_SLOT": "1",
+            "DSX_SCAN_LINE": "1", "DSX_SCAN_TRACE": "0", "DSX_WAVE_MAJOR": "1",
+            "DSX_FIXUP_FAST": "1", "DSX_FINISH": "1", "DSX_SEG_MAX": "4", "DSX_SEG_TARGET": "4096",
+            "DSX_DIGEST_PF": "1", "DSX_TAIL_MULT": "1", "DSX_LANE_BYTES": None,
+            "DSX_STITCH_CUS": "0", "DSX_SCAN_MASK": "0", "DSX_SCAN_PRIO": None,
+            "DSX_STREAM_BATCH": None, "DSX_NOOP_BEFORE_SCAN": None}
+
+
 def lib():
     """Load libdsx.so; raises ImportError if it has not been built."""
     global _lib
@@ -148,13 +166,12 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                 "(make -C desync_amd/csrc). desync_amd has no CPU fallback.")
-        diag_env = [k for k in ("DSX_SCAN_VARIANT", "DSX_SCAN_CFG", "DSX_FUSE")
-                    if os.environ.get(k, "0") not in ("", "0")]
+        diag_env = [k for k, dflt in DIAG_ENV.items() if os.environ.get(k, "") not in ("", dflt)]
         if diag_env and not os.path.basename(LIB_PATH).startswith("libdsx_diag"):
             raise ImportError(
-                f"{', '.join(diag_env)} selects a diagnostic kernel path (scan ablations, "
-                "other geometries, the stitch behind the scan), which only the diagnostic "
-                "build holds: make -C desync_amd/csrc diag and set "
+                f"{', '.join(diag_env)} selects a diagnostic path (scan ablations, other "
+                "geometries, rejected experiments), which only the diagnostic build reads: "
+                "make -C desync_amd/csrc diag and set "
                 "DSX_LIB_PATH=desync_amd/libdsx_diag.so")
         _share_torch_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)

@@ -73,3 +73,59 @@ def test_seam_record_layout():
     has the C layout (static_assert in dsx_api.cpp)."""
     assert ctypes.sizeof(_lib.Seam) == 7 * 8 + 4 * 4 + 8 * (1024 + 1024)
     assert _lib.Seam.cands.offset == 7 * 8 + 4 * 4
+
+
+# Message tokens that appear as text in the library (error strings), not as
+# environment settings it reads.
+_MESSAGE_TOKENS = {"DSX_NO_SYNC", "DSX_SEAM_ERROR", "DSX_SEAM_MAX_CUTS"}
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _dsx_strings(path):
+    with open(path, "rb") as f:
+        return {m.decode() for m in re.findall(rb"DSX_[A-Z0-9_]+", f.read())}
+
+
+def test_product_library_reads_only_the_documented_environment():
+    """libdsx.so names exactly _lib.PRODUCT_ENV: the
+    rejected experiments and diagnostic geometries are compiled into
+    libdsx_diag.so only.  INTEGRATION.md documents each product setting, a
+    test sets each one, and loading the product library refuses a
+    diagnostic setting instead of ignoring it."""
+    names = _dsx_strings(_lib.LIB_PATH) - _MESSAGE_TOKENS
+    assert names == set(_lib.PRODUCT_ENV), sorted(names ^ set(_lib.PRODUCT_ENV))
+    doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    env_doc = doc[doc.index("## Environment"):]
+    tests = "".join(open(os.path.join(REPO, "tests", f)).read()
+                    for f in os.listdir(os.path.join(REPO, "tests"))
+                    if f.endswith(".py") and f != "test_abi.py")
+    for k in _lib.PRODUCT_ENV:
+        assert f"`{k}`" in env_doc, k
+        assert f'"{k}"' in tests, f"{k}: no test sets it"
+    assert not set(_lib.DIAG_ENV) & set(_lib.PRODUCT_ENV)
+
+
+def test_diagnostic_library_reads_the_diagnostic_environment():
+    diag = os.path.join(REPO, "desync_amd", "libdsx_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("libdsx_diag.so not built (make -C desync_amd/csrc diag)")
+    names = _dsx_strings(diag) - _MESSAGE_TOKENS
+    assert set(_lib.DIAG_ENV) | set(_lib.PRODUCT_ENV) == names, sorted(
+        names ^ (set(_lib.DIAG_ENV) | set(_lib.PRODUCT_ENV)))
+
+
+def test_diagnostic_setting_refused_by_the_product_library():
+    import subprocess
+    import sys
+    for k, v in (("DSX_PREFETCH", "1"), ("DSX_SCAN_TRACE", "1"), ("DSX_WAVE_MAJOR", "0")):
+        env = dict(os.environ, **{k: v})
+        env.pop("DSX_LIB_PATH", None)
+        r = subprocess.run([sys.executable, "-c", "from desync_amd import _lib; _lib.lib()"],
+                           env=env, capture_output=True, text=True, timeout=120, cwd=REPO)
+        assert r.returncode != 0 and k in r.stderr and "libdsx_diag" in r.stderr, (k, r.stderr)
+    # the value the product library behaves as is accepted
+    env = dict(os.environ, DSX_FUSE="0", DSX_WAVE_MAJOR="1")
+    env.pop("DSX_LIB_PATH", None)
+    r = subprocess.run([sys.executable, "-c", "from desync_amd import _lib; _lib.lib()"],
+                       env=env, capture_output=True, text=True, timeout=120, cwd=REPO)
+    assert r.returncode == 0, r.stderr

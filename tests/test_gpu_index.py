@@ -75,6 +75,33 @@ def test_index_fd_many_windows(tmp_path, monkeypatch, algo, kind):
     assert [bytes(x) for x in ids] == _ids(data, ref, algo)
 
 
+@pytest.mark.parametrize("readers", ["1", "7"])
+def test_index_fd_reader_threads(tmp_path, monkeypatch, readers):
+    """DSX_INDEX_READERS: one reader thread, and more threads than the 4
+    pinned slots a 1 MiB window needs, fill the slots out of order; the cut
+    list and IDs are the same."""
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_INDEX_READERS", readers)
+    monkeypatch.setenv("DSX_INDEX_WINDOW", str(1 << 20))
+    monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 18))
+    data = o.synth_uniform(43, 0, (24 << 20) + 4321)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ctx = _lib.Context(0)
+    try:
+        fd = os.open(str(f), os.O_RDONLY)
+        try:
+            ends, ids = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+        finally:
+            os.close(fd)
+    finally:
+        ctx.close()
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    assert np.array_equal(ends, ref)
+    assert [bytes(x) for x in ids] == _ids(data, ref, "sha512-256")
+
+
 def test_index_host_two_gib_windows():
     """1.5 GiB through the default 1 GiB windows (two of them): every cut
     against oracle.chunk_parallel, every ID against hashlib."""

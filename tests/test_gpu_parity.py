@@ -234,13 +234,12 @@ def test_random_avg_sweep(dctx, avg):
     assert np.array_equal(gpu_cut(dctx, data, mn, avg, mx), o.chunk_stream(data, mn, avg, mx))
 
 
-@pytest.mark.parametrize("env", [{"DSX_LANE_TARGET": "384"}, {"DSX_LANE_TARGET": "2304"},
-                                 {"DSX_SCAN_LINE": "0"}, {"DSX_WAVE_MAJOR": "0"}])
+@pytest.mark.parametrize("env", [{"DSX_LANE_TARGET": "384"}, {"DSX_LANE_TARGET": "2304"}, {}])
 def test_scan_geometries(env, monkeypatch):
-    """The line-aligned scan with short lane segments (many regions per wave
-    slot from the work queue), the 96-B-row scan_kernel, and device pointers
-    off the 128-B line grid: at the blob start (scan_kernel fallback) and
-    inside it (shard pieces: grid origin before the piece start)."""
+    """The line-aligned scan with short lane segments (DSX_LANE_TARGET: many
+    regions per wave slot from the work queue) and device pointers off the
+    128-B line grid: at the blob start (the 96-B-row scan_kernel) and inside
+    it (shard pieces: grid origin before the piece start)."""
     import torch
     import desync_amd
     from desync_amd import _lib

@@ -4,6 +4,8 @@ the trace of the last queued scan).  DESIGN.md 4.2."""
 import ctypes, os, sys
 import numpy as np
 os.environ["DSX_SCAN_TRACE"] = "1"
+os.environ.setdefault("DSX_LIB_PATH", os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "desync_amd", "libdsx_diag.so"))  # traces: the diagnostic build
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import desync_amd

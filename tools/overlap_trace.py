@@ -11,6 +11,8 @@ import sys
 import numpy as np
 
 os.environ["DSX_SCAN_TRACE"] = "2"
+os.environ.setdefault("DSX_LIB_PATH", os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "desync_amd", "libdsx_diag.so"))  # traces: the diagnostic build
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 from desync_amd import _lib  # noqa: E402

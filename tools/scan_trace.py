@@ -9,9 +9,8 @@ import sys
 import numpy as np
 
 os.environ["DSX_SCAN_TRACE"] = "1"
-if os.environ.get("DSX_SCAN_VARIANT", "0") != "0":  # VARIANT 5: the diagnostic build
-    os.environ.setdefault("DSX_LIB_PATH", os.path.join(
-        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "desync_amd", "libdsx_diag.so"))
+os.environ.setdefault("DSX_LIB_PATH", os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "desync_amd", "libdsx_diag.so"))  # traces: the diagnostic build
 print("scan_trace: importing torch", flush=True)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
