@@ -22,6 +22,7 @@ buffer with readinto when the reader has it) and hands out confirmed chunks.
 """
 from __future__ import annotations
 
+import bisect
 import ctypes
 import itertools
 
@@ -201,10 +202,10 @@ class Chunker:
         q, qi, n = self._q, self._qi, len(self._q)
         if qi >= n or self._win is None:
             return out
-        mx, R, ra, pos = self.params.max, self._R, self._ra, self._pos
         win, wb, ids = self._win, self._wbase, self._qids if self._idbuf is not None else None
         cur = self._cur
-        while qi < n and R - cur >= mx and not (ra and pos - cur < ra // 2):
+        k = self._run_end()
+        while qi < k:
             e = q[qi]
             out.append((cur, win[cur - wb:e - wb].tobytes(),
                         ids[32 * qi:32 * qi + 32] if ids is not None else None))
@@ -214,6 +215,57 @@ class Chunker:
         if ids is not None:
             self._last_id = out[-1][2]
         return out
+
+    def _run_end(self):
+        """After a Next() that took chunk qi-1 from the popped queue: the end
+        k of the run of queued chunks qi..k-1 that Next() would return without
+        reading.  Chunk j starts at q[j-1] and is in the run while the
+        reference's fillBuffer check would not read (start <= R - max) and
+        the read-ahead is not due (start <= pos - ra/2); starts only grow, so
+        one bisection.  At the end of the stream (no read can happen, no
+        reader error pending) fillBuffer only moves R: the whole queue is the
+        run, and R moves as Next() would move it."""
+        q, qi, n = self._q, self._qi, len(self._q)
+        mx = self.params.max
+        if self._eof and self._err is None:
+            R = self._R
+            for j in range(qi, n):
+                if R - q[j - 1] < mx:
+                    R = q[j - 1] + 10 * mx
+            self._R = R
+            return n
+        limit = self._R - mx
+        if self._ra:
+            limit = min(limit, self._pos - self._ra // 2)
+        return min(n, bisect.bisect_right(q, limit, qi - 1, n) + 1)
+
+    def _next_block(self, clone=None, max_bytes=None):
+        """_next_run's chunks as one block, with no per-chunk object: (start,
+        ends, ids, data) -- ends the chunks' absolute end offsets (a list),
+        ids their 32-byte IDs concatenated (b"" without IDs), data ONE copy
+        of [start, ends[-1]) (``clone(view)`` of the library's bytes, default
+        bytes(view)) -- or None at the end of the stream.  The same chunks as
+        _next_run, up to the same point (the reference's fillBuffer check or
+        the read-ahead) or max_bytes; the first comes from Next()."""
+        clone = clone or bytes
+        s, b = self.Next()
+        if not b:
+            return None
+        q, qi, n = self._q, self._qi, len(self._q)
+        ids = self._qids if self._idbuf is not None else None
+        if qi >= n or self._win is None:
+            return s, [s + len(b)], self._last_id or b"", clone(b)
+        k = self._run_end()
+        if max_bytes is not None:  # (at least the first chunk)
+            k = max(qi, min(k, bisect.bisect_right(q, s + max_bytes, qi - 1, k)))
+        end = q[k - 1]
+        first = qi - 1
+        data = clone(self._win[s - self._wbase:end - self._wbase])
+        idb = ids[32 * first:32 * k] if ids is not None else b""
+        self._qi, self._cur = k, end
+        if ids is not None:
+            self._last_id = ids[32 * (k - 1):32 * k]
+        return s, q[first:k], idb, data
 
     def EnableIDs(self, algo=None):
         """Compute every chunk's Digest.Sum on the GPU next to its cut (for

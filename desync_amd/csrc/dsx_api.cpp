@@ -201,6 +201,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_FUSE")) c->fuse = atoi(v) != 0;
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_TARGET")) c->seg_target = (uint64_t)std::max(0L, atol(v));
+  if (const char* v = getenv("DSX_WALK_WGS")) c->walk_wgs = std::max(1, std::min(4, atoi(v)));
   if (const char* v = getenv("DSX_DIGEST_PF")) c->digest_pf = atoi(v) != 0;
   if (const char* v = getenv("DSX_TAIL_MULT")) c->tail_mult = std::max(1, std::min(4, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
@@ -955,14 +956,17 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   const double exp_per_seg = (double)seg / (double)p->discriminator + 8.0;
   // segments per walk workgroup: about two workgroups per CU (the walks are
   // latency-bound), within the LDS candidate and region budgets
-  uint64_t spg = std::max<uint64_t>(2, nseg / (2ull * (uint64_t)c->ncu));
+  uint64_t spg = std::max<uint64_t>(2, nseg / ((uint64_t)c->walk_wgs * (uint64_t)c->ncu));
   // split streams: the walk runs beside the next piece's scan on the CUs the
   // scan leaves free, two 1024-thread workgroups per CU (LDS: ~69 KiB each)
   const bool wide = c->scan_stream != c->stream;
   if (wide)
     spg = std::max<uint64_t>(spg, (nseg + 2ull * c->stitch_cus - 1) / (2ull * c->stitch_cus));
   spg = std::min<uint64_t>(spg, (uint64_t)((double)kWalkLdsCap / (2.0 * exp_per_seg)) - 1);
-  const uint64_t max_spg_reg = region_bytes ? (4000ull * region_bytes) / seg : kMaxSpg;
+  // (the smaller region size bounds the regions a workgroup's span covers:
+  // two region sizes put the short tail regions at the piece's end)
+  const uint64_t rb_min = pc.RB2 ? std::min<uint64_t>(region_bytes, pc.RB2) : region_bytes;
+  const uint64_t max_spg_reg = rb_min ? (4000ull * rb_min) / seg : kMaxSpg;
   spg = std::min<uint64_t>(spg, max_spg_reg > 2 ? max_spg_reg - 2 : 1);
   spg = std::max<uint64_t>(1, std::min<uint64_t>(spg, kMaxSpg));
   ta.spg = (uint32_t)spg;

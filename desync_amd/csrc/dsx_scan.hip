@@ -1135,6 +1135,16 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
             // chunker.go:265's test is t - qBias <= qMax with no rotate
 #pragma unroll
             for (int q = 0; q < 8; ++q) bits |= (t[q] - tcv.qbias <= tcv.qmax ? 1u : 0u) << q;
+          } else if (MODE == 2) {
+            // even d = 2^k * dodd: chunker.go:265's test on the same product,
+            // rotl((h+1)*inv, -k) - qBias <= qMax -- one v_alignbit more
+            // per byte instead of mode2_exact's two multiplies (the prefilter
+            // passes 2^k times the candidates: this path runs 2^k times as
+            // often as for an odd d of the same size)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              bits |= (__builtin_amdgcn_alignbit(t[q], t[q], tcv.rot) - tcv.qbias <= tcv.qmax ? 1u : 0u)
+                      << q;
           } else {
 #pragma unroll
             for (int q = 0; q < 8; ++q) {

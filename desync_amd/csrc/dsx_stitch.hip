@@ -236,14 +236,17 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
 
   const uint32_t nwalk = kB - kFirst + 1;
   const RelChain rc = rel_chain(a.chain, lo);
-  const bool record = nwalk * a.scap <= kSpecLds;
+  // LDS slots per recorded speculative chain (a chain longer than that is not
+  // recorded: phase 2 then walks its segment in full)
+  const uint32_t stride = min(a.scap, kSpecLds / nwalk);
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   constexpr uint32_t kWaves = kWalkThreads / 64;
   // ---- phase 1: speculative chain of each segment -> exit X_k (one wave each) ----
   // A chain step is a ballot over the 64 candidates the wave holds in a
   // register, s_ff1 and a readlane; the chain's cuts go into one register
-  // (lane i = cut i) and to LDS once at the end, so no step
-  // waits on LDS (each step's LDS store used to cost an lgkmcnt(0) wait).
+  // (lane i = cut 64j + i) and to LDS once per 64 cuts, so no step waits on
+  // LDS (each step's LDS store used to cost an lgkmcnt(0) wait).  Chains of
+  // more than 64 cuts (avg 16 KiB: ~128 per 2 MiB segment) are recorded too.
   // (One lane per chain, a cursor into the LDS candidates, was slower: 37.1
   // against 31.4 us per 8 GiB piece, its steps wait on dependent LDS reads;
   // profiles/r04r.)
@@ -271,15 +274,17 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
           if (nx == kRelUndet) why = 2;
           break;
         }
-        specv = ln == ns ? nx : specv;  // (v_cmp + v_cndmask; no lane >= 64)
+        specv = ln == (ns & 63u) ? nx : specv;  // (v_cmp + v_cndmask)
         ++ns;
+        if (__builtin_expect((ns & 63u) == 0u, 0) && ns <= stride)  // a full block of 64
+          s_spec[t * stride + ns - 64u + ln] = specv;
         last = nx;
         x = nx;
       }
       if (tr && t == wv) tr[9] = __builtin_amdgcn_s_memrealtime();
-      // (more than 64 cuts, or more than the LDS holds: no phase-2 shortcut)
-      const bool keep = record && ns <= 64u && ns <= a.scap;
-      if (keep && ln < ns) s_spec[t * a.scap + ln] = specv;
+      // (more cuts than the chain's LDS slots: no phase-2 shortcut)
+      const bool keep = ns <= stride;
+      if (keep && ln < (ns & 63u)) s_spec[t * stride + (ns & ~63u) + ln] = specv;
       if (ln == 0) {
         xs[t] = lo + last;
         s_spec_n[t] = keep ? ns : 0xFFFFFFFFu;
@@ -321,10 +326,12 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
     uint32_t n = 0, flags = 0;
     const uint32_t er = rel_clamp(e, lo), sr = rel_clamp(sst, lo);
     uint32_t x = rel_clamp(E, lo), last = x;
-    // the speculative chain of this segment (phase 1), one cut per lane
-    const uint32_t sn = record ? s_spec_n[t] : 0xFFFFFFFFu;
+    // the speculative chain of this segment (phase 1): its first 64 cuts, one
+    // per lane (the chains meet within the first few cuts, or not at all)
+    const uint32_t sn = s_spec_n[t];
     const bool have_spec = sn != 0xFFFFFFFFu;
-    const uint32_t specv = have_spec && ln < sn ? s_spec[t * a.scap + ln] : 0xFFFFFFFFu;
+    const uint32_t* spec = s_spec + t * stride;
+    const uint32_t specv = have_spec && ln < sn ? spec[ln] : 0xFFFFFFFFu;
     while (true) {
       uint32_t nx;
       if (__builtin_expect(x >= rc.tail_at, 0)) {  // (tail_at <= end_at)
@@ -350,9 +357,10 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
           // chain continues with its cuts and ends the way it ended
           const uint32_t f = (uint32_t)__builtin_ctzll(hit);
           const uint32_t rest = sn - f - 1;
-          if (ln > f && ln < sn && n + (ln - f - 1) < a.scap) out[n + (ln - f - 1)] = lo + specv;
+          for (uint32_t j = f + 1u + ln; j < sn; j += 64u)
+            if (n + (j - f - 1u) < a.scap) out[n + (j - f - 1u)] = lo + spec[j];
           n += rest;
-          if (rest) last = (uint32_t)__builtin_amdgcn_readlane((int)specv, (int)(sn - 1));
+          if (rest) last = spec[sn - 1u];
           if (s_spec_end[t] == 1) flags |= kSegEnd;
           if (s_spec_end[t] == 2) flags |= kSegUndet;
           break;

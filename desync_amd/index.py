@@ -50,14 +50,16 @@ class ChunkArray(MutableSequence):
     when an element is read, and WriteTo packs the arrays directly.  Any
     change turns it into a plain list of IndexChunk first."""
 
-    def __init__(self, ends, ids):
+    def __init__(self, ends, ids, start=0):
         self._ends = np.ascontiguousarray(ends, dtype=np.uint64)
+        ids = np.frombuffer(ids, dtype=np.uint8) if isinstance(ids, (bytes, bytearray)) else ids
         self._ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 32)
+        self._start = int(start)  # the first chunk's start (the stream position it began at)
         self._list = None
 
     def _chunk(self, i):
         e = int(self._ends[i])
-        s = int(self._ends[i - 1]) if i else 0
+        s = int(self._ends[i - 1]) if i else self._start
         return IndexChunk(self._ids[i].tobytes(), s, e - s)
 
     def _materialize(self):
@@ -65,7 +67,7 @@ class ChunkArray(MutableSequence):
             el = self._ends.tolist()
             raw = self._ids.tobytes()
             self._list = [IndexChunk(raw[32 * i:32 * i + 32], s, e - s)
-                          for i, (s, e) in enumerate(zip([0] + el[:-1], el))]
+                          for i, (s, e) in enumerate(zip([self._start] + el[:-1], el))]
         return self._list
 
     def __len__(self):

@@ -438,6 +438,44 @@ def test_chunker_runs_equal_next():
         assert got == want and runs < len(want)
 
 
+def test_chunker_blocks_equal_next():
+    """Chunker._next_block (ChunkStream's path: one block of ends, IDs and a
+    single clone of the bytes per run) describes exactly Next()'s (start,
+    bytes, ID) sequence, with IDs on and off and with the read-ahead, across
+    8 MiB reads, a zero run and a 10*max refill boundary."""
+    import desync_amd
+    data = np.concatenate([o.synth_uniform(48, 0, 40 << 20), np.zeros(2 << 20, np.uint8),
+                           o.synth_uniform(49, 0, (9 << 20) + 3)]).tobytes()
+    for ids, ra in ((False, 0), (True, 0), (True, 256 << 20)):
+        a = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX)
+        b = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX)
+        if ids:
+            a.EnableIDs()
+            b.EnableIDs()
+        b._ra = ra
+        want = []
+        while True:
+            s, chunk = a.Next()
+            if not chunk:
+                break
+            want.append((s, bytes(chunk), a.ChunkID()))
+        got, blocks = [], 0
+        while True:
+            blk = b._next_block()
+            if blk is None:
+                break
+            blocks += 1
+            s0, ends, idb, raw = blk
+            assert len(raw) == ends[-1] - s0 and len(idb) == (32 * len(ends) if ids else 0)
+            s = s0
+            for i, e in enumerate(ends):
+                got.append((s, raw[s - s0:e - s0], idb[32 * i:32 * i + 32] if ids else None))
+                s = e
+        a.close()
+        b.close()
+        assert got == want and blocks < len(want)
+
+
 def test_chunk_stream_errors():
     """A failing store raises out of ChunkStream; a cancelled ctx stops the
     producer and returns the chunks so far (index.go:203-206)."""

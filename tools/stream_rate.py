@@ -57,7 +57,7 @@ def main():
             object.__setattr__(self, "_c", c)
 
         def __getattr__(self, k):
-            if k == "_next_run":
+            if k in ("_next_run", "_next_block"):
                 raise AttributeError(k)
             return getattr(self._c, k)
 
