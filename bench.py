@@ -205,6 +205,8 @@ def cpu_baseline(host_blob, threads=None):
                    f"n=10 (desync make default): {rate10:.3f} GiB/s over {reps10}x; "
                    f"single thread {single:.3f} GiB/s on 128 MiB; SHA-512/256 IDs "
                    f"{ids:.3f} GiB/s over {threads} threads on 256 MiB"),
+        "bytes": int(n),
+        "gpu_bytes_per_step": None,
         "n10_gibs": round(rate10, 3),
         "single_thread_gibs": round(single, 3),
         "ids_sha512_256_gibs": round(ids, 3),
@@ -488,6 +490,7 @@ def main():
             # a bounded sample: the shard's first GiB (the leg is ~10-30 s of CPU work)
             host = blob[halo:halo + min(n, CPU_SAMPLE)].cpu().numpy()
             res["cpu_baseline"] = cpu_baseline(host, args.cpu_threads or None)
+            res["cpu_baseline"]["gpu_bytes_per_step"] = n  # (the sample is the shard's first GiB)
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -930,9 +930,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   if (!live) {
     if (a.stamp) stamp_end(a.stamp, s_stamp, wave);
 #if DSX_DIAG
-  #if DSX_DIAG
-  if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
-#endif
+    if constexpr (FUSE) run_tasks(a.tasks, reinterpret_cast<uint32_t*>(stage), lane, task_tr);
 #endif
     return;
   }
@@ -1287,7 +1285,9 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
     // the lane before reports them as S + 1 .. S + 48, lane 63 excepted)
     const uint32_t ext = lane < 63u ? (uint32_t)kHandoff : 0u;
     if (lane > 0u && lo < (int64_t)kHandoff + 1) lo = (int64_t)kHandoff + 1;
-    const uint32_t o_min = lo <= 1 ? 1u : (lo > (int64_t)S ? S + 1u : (uint32_t)lo);
+    // (clamped past the extension too: a lane wholly before min_pos reports
+    // none of the handoff positions S + 1 .. S + ext either)
+    const uint32_t o_min = lo <= 1 ? 1u : (lo > (int64_t)(S + ext) ? S + ext + 1u : (uint32_t)lo);
     const int64_t hi = (int64_t)a.len - lane_p;
     const uint32_t o_max = hi <= 0 ? 0u : (hi >= (int64_t)(S + ext) ? S + ext : (uint32_t)hi);
     const uint32_t n = cnt < a.lane_slots + kHitRegs ? cnt : a.lane_slots + kHitRegs;
