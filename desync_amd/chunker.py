@@ -248,7 +248,11 @@ class Chunker:
         _next_run, up to the same point (the reference's fillBuffer check or
         the read-ahead) or max_bytes; the first comes from Next()."""
         clone = clone or bytes
-        s, b = self.Next()
+        zc, self._zero_copy = self._zero_copy, True  # (the first chunk: a view, cloned below)
+        try:
+            s, b = self.Next()
+        finally:
+            self._zero_copy = zc
         if not b:
             return None
         q, qi, n = self._q, self._qi, len(self._q)

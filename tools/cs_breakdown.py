@@ -68,6 +68,20 @@ def main():
         ch.close()
         return len(out)
 
+    def blocks_only():  # ChunkStream's producer side: blocks with IDs, no store threads
+        from desync_amd.stream import _ClonePool, _SLAB
+        ch = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX)
+        ch.EnableIDs()
+        ch._ra = 256 << 20
+        pool, k = _ClonePool(8), 0
+        while True:
+            blk = ch._next_block(pool.clone, _SLAB)
+            if blk is None:
+                break
+            k += len(blk[1])
+        ch.close()
+        return k
+
     from desync_amd import _lib
     shared = _lib.Context(0)
 
@@ -79,7 +93,7 @@ def main():
 
     res = {"tool": "cs_breakdown", "mib": mib}
     for name, fn in (("next", lambda: next_only(False)), ("next_ids", lambda: next_only(True)),
-                     ("producer", producer_only), ("chunkstream_1", lambda: cs(1)),
+                     ("producer", producer_only), ("blocks", blocks_only), ("chunkstream_1", lambda: cs(1)),
                      ("chunkstream_4", lambda: cs(4)),
                      ("cs4_shared", lambda: cs(4, shared))):
         fn()  # warm-up
