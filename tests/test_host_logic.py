@@ -188,3 +188,74 @@ def test_context_pool(monkeypatch):
     assert _lib.acquire_context(0) is idle[-1]
     n = len(made)
     assert _lib.acquire_context(0) not in many and len(made) == n + 1
+
+
+def test_clone_pool_reuses_released_slabs():
+    """ChunkStream's clones (desync_amd.stream._ClonePool): a slab returns to
+    the pool once the last chunk view of it is gone, a store that keeps its
+    chunks' bytes makes the pool fall back to fresh copies, and every clone is
+    a read-only copy of its source."""
+    import gc
+
+    import numpy as np
+
+    from desync_amd import stream
+    pool = stream._ClonePool(2)
+    src = np.arange(1 << 20, dtype=np.uint64).view(np.uint8)
+    a = pool.clone(memoryview(src))
+    assert a.readonly and bytes(a[:64]) == src[:64].tobytes() and len(a) == src.size
+    base_a = a.obj.base
+    b = pool.clone(memoryview(src[:4096]))  # the second (and last) slab
+    kept = b[100:200]  # a store keeping a chunk view holds b's slab
+    del a
+    gc.collect()
+    c = pool.clone(memoryview(src[:8192]))  # a's slab, released
+    assert c.obj.base is base_a
+    d = pool.clone(memoryview(src[:16]))  # no free slab: a fresh copy
+    assert isinstance(d.obj, bytes) and bytes(d) == src[:16].tobytes()
+    assert bytes(kept) == src[100:200].tobytes()
+    big = pool.clone(memoryview(np.zeros(stream._SLAB + 1, np.uint8)))  # larger than a slab
+    assert isinstance(big.obj, bytes) and len(big) == stream._SLAB + 1
+
+
+def test_chunk_array_start():
+    """Index.Chunks as a ChunkArray whose first chunk starts past 0 (a stream
+    that began at an offset): Start/Size of each element, materialised or
+    not, and the caibx table of absolute chunk ends."""
+    import numpy as np
+
+    from desync_amd.index import ChunkArray
+    ends = np.array([1500, 4000, 4100], np.uint64)
+    ids = bytes(range(96))
+    ca = ChunkArray(ends, ids, start=1000)
+    assert (ca[0].Start, ca[0].Size) == (1000, 500) and ca[2].ID == bytes(range(64, 96))
+    assert [(c.Start, c.Size) for c in ca] == [(1000, 500), (1500, 2500), (4000, 100)]
+
+
+def test_smu_summary_window():
+    """tools/smu_summary.py over synthetic SMU samples: energy from the
+    accumulator over the --marks window, J/GiB above idle, PPT residency from
+    the accumulation counters."""
+    import importlib.util
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                        "smu_summary.py")
+    spec = importlib.util.spec_from_file_location("smu_summary", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rows, e, t0 = [], 0.0, 1000.0
+    for i in range(2000):  # 2 ms samples: 0.4 s idle at 250 W, 2 s at 1400 W, idle again
+        t = t0 + 0.002 * i
+        p = 1400.0 if 0.4 <= t - t0 < 2.4 else 250.0
+        e += p * 0.002 / 15.259e-6
+        r = {"t": t, "current_socket_power": p, "energy_accumulator": int(e),
+             "accumulation_counter": i, "ppt_residency_acc": min(max(i - 200, 0), 400)}
+        rows.append(r)
+    static = {"energy": {"counter_resolution": 15.259}}
+    out = mod.summarise(static, rows, {"t0": t0 + 0.5, "t1": t0 + 2.0, "bytes": 3 << 30})
+    json.dumps(out)
+    assert abs(out["mean_power_w"] - 1400) < 2 and out["idle_w"] == 250.0
+    assert abs(out["j_per_gib"] - 1400 * 1.5 / 3) < 1
+    assert abs(out["j_per_gib_above_idle"] - 1150 * 1.5 / 3) < 1
+    assert abs(out["res_ppt"] - 350 / 750) < 0.01  # (PPT active over samples 200..599)
