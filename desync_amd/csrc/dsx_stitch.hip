@@ -261,8 +261,32 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
       const uint32_t er = rel_clamp(e, lo);
       uint32_t x = rel_clamp(v, lo), last = x;
       uint32_t ns = 0, why = 0;
-      uint32_t specv = 0;  // lane i: the chain's i-th cut (i < 64)
+      uint32_t specv = 0;  // lane i: the chain's cut 64j + i
+      const uint32_t cap = min(rc.lim_cap, er);  // (the common step's bound: chunker.go:221, the segment)
+      auto record = [&](uint32_t c) __attribute__((always_inline)) {
+        specv = ln == (ns & 63u) ? c : specv;  // (v_cmp + v_cndmask)
+        ++ns;
+        if (__builtin_expect((ns & 63u) == 0u, 0) && ns <= stride)  // a full block of 64
+          s_spec[t * stride + ns - 64u + ln] = specv;
+        last = c;
+        x = c;
+      };
       while (true) {
+        // The common step, with one exit for everything else: the next
+        // candidate in the register window past x + min is the next cut
+        // (chunker.go:259-271) when it lies within x + max and the segment
+        // (round 5: a loop with a single rare exit compiles to about half the
+        // scalar instructions of rel_step's folded form)
+        if (x < rc.tail_at) {
+          uint64_t m = __ballot(src.v > x + rc.min);
+          while (m != 0) {  // (m == 0: window exhausted, rel_step refills)
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)src.v, (int)__builtin_ctzll(m));
+            if (__builtin_expect(c > min(x + rc.max, cap), 0)) break;
+            record(c);
+            if (__builtin_expect(x >= rc.tail_at, 0)) break;
+            m = __ballot(src.v > x + rc.min);
+          }
+        }
         uint32_t nx;
         if (__builtin_expect(x >= rc.tail_at, 0)) {  // (tail_at <= end_at)
           if (x >= rc.end_at) { why = 1; break; }
@@ -274,12 +298,7 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
           if (nx == kRelUndet) why = 2;
           break;
         }
-        specv = ln == (ns & 63u) ? nx : specv;  // (v_cmp + v_cndmask)
-        ++ns;
-        if (__builtin_expect((ns & 63u) == 0u, 0) && ns <= stride)  // a full block of 64
-          s_spec[t * stride + ns - 64u + ln] = specv;
-        last = nx;
-        x = nx;
+        record(nx);
       }
       if (tr && t == wv) tr[9] = __builtin_amdgcn_s_memrealtime();
       // (more cuts than the chain's LDS slots: no phase-2 shortcut)
