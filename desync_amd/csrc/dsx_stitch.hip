@@ -243,10 +243,11 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
   constexpr uint32_t kWaves = kWalkThreads / 64;
   // ---- phase 1: speculative chain of each segment -> exit X_k (one wave each) ----
   // A chain step is a ballot over the 64 candidates the wave holds in a
-  // register, s_ff1 and a readlane; the chain's cuts go into one register
-  // (lane i = cut 64j + i) and to LDS once per 64 cuts, so no step waits on
-  // LDS (each step's LDS store used to cost an lgkmcnt(0) wait).  Chains of
-  // more than 64 cuts (avg 16 KiB: ~128 per 2 MiB segment) are recorded too.
+  // register, s_ff1 and a readlane; the chain's cuts are bits of a scalar
+  // mask over the window's lanes and go to LDS once per window, so no step
+  // waits on LDS (each step's LDS store used to cost an lgkmcnt(0) wait).
+  // Chains of any length up to the LDS slots are recorded (avg 16 KiB: ~128
+  // cuts per 2 MiB segment).
   // (One lane per chain, a cursor into the LDS candidates, was slower: 37.1
   // against 31.4 us per 8 GiB piece, its steps wait on dependent LDS reads;
   // profiles/r04r.)
@@ -259,34 +260,43 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
       src.seek(v);
       if (tr && t == wv) tr[7] = __builtin_amdgcn_s_memrealtime();
       const uint32_t er = rel_clamp(e, lo);
-      uint32_t x = rel_clamp(v, lo), last = x;
+      uint32_t x = rel_clamp(v, lo);
       uint32_t ns = 0, why = 0;
-      uint32_t specv = 0;  // lane i: the chain's cut 64j + i
-      const uint32_t cap = min(rc.lim_cap, er);  // (the common step's bound: chunker.go:221, the segment)
-      auto record = [&](uint32_t c) __attribute__((always_inline)) {
-        specv = ln == (ns & 63u) ? c : specv;  // (v_cmp + v_cndmask)
-        ++ns;
-        if (__builtin_expect((ns & 63u) == 0u, 0) && ns <= stride)  // a full block of 64
-          s_spec[t * stride + ns - 64u + ln] = specv;
-        last = c;
-        x = c;
+      uint32_t* spec_t = s_spec + t * stride;
+      // The common step's bound: chunker.go:221's limit, the segment end, and
+      // below the last piece's tail (chunker.go:215-217), so a common step
+      // never needs the tail test.
+      const uint32_t cap = __builtin_amdgcn_readfirstlane(rc.tail_at ? min(min(rc.lim_cap, er), rc.tail_at - 1u) : 0u);
+      // window lanes cut since the last flush: a common step records its cut
+      // with one scalar bit-set; the cuts reach LDS once per window, in order
+      uint64_t cm = 0;
+      auto flush = [&]() __attribute__((always_inline)) {
+        if (cm) {
+          const uint32_t idx = ns + __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+          if (((cm >> ln) & 1u) && idx < stride) spec_t[idx] = src.v;
+          ns += (uint32_t)__builtin_popcountll(cm);
+          cm = 0;
+        }
       };
       while (true) {
         // The common step, with one exit for everything else: the next
         // candidate in the register window past x + min is the next cut
-        // (chunker.go:259-271) when it lies within x + max and the segment
-        // (round 5: a loop with a single rare exit compiles to about half the
-        // scalar instructions of rel_step's folded form)
+        // (chunker.go:259-271) when it lies within x + max and below `cap`
+        // (round 5: ballot, s_ff1, readlane, one compare and a bit-set;
+        // DESIGN.md 4.2)
         if (x < rc.tail_at) {
           uint64_t m = __ballot(src.v > x + rc.min);
           while (m != 0) {  // (m == 0: window exhausted, rel_step refills)
-            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)src.v, (int)__builtin_ctzll(m));
+            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)src.v, (int)l);
             if (__builtin_expect(c > min(x + rc.max, cap), 0)) break;
-            record(c);
-            if (__builtin_expect(x >= rc.tail_at, 0)) break;
+            cm |= 1ull << l;
+            x = c;
             m = __ballot(src.v > x + rc.min);
           }
         }
+        flush();  // (before rel_step moves the window)
         uint32_t nx;
         if (__builtin_expect(x >= rc.tail_at, 0)) {  // (tail_at <= end_at)
           if (x >= rc.end_at) { why = 1; break; }
@@ -298,17 +308,18 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
           if (nx == kRelUndet) why = 2;
           break;
         }
-        record(nx);
+        if (ln == 0 && ns < stride) spec_t[ns] = nx;  // a rare step's cut
+        ++ns;
+        x = nx;
       }
       if (tr && t == wv) tr[9] = __builtin_amdgcn_s_memrealtime();
       // (more cuts than the chain's LDS slots: no phase-2 shortcut)
       const bool keep = ns <= stride;
-      if (keep && ln < (ns & 63u)) s_spec[t * stride + (ns & ~63u) + ln] = specv;
       if (ln == 0) {
-        xs[t] = lo + last;
+        xs[t] = lo + x;
         s_spec_n[t] = keep ? ns : 0xFFFFFFFFu;
         s_spec_end[t] = why;
-        if (k >= kA) a.seg_info[k].X = lo + last;  // kA-1 belongs to the previous workgroup
+        if (k >= kA) a.seg_info[k].X = lo + x;  // kA-1 belongs to the previous workgroup
       }
     }
   }

@@ -18,6 +18,7 @@ import desync_amd  # noqa: E402
 from desync_amd import _lib  # noqa: E402
 
 gib = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
+avg = int(sys.argv[2]) << 10 if len(sys.argv) > 2 else 65536  # (KiB; min = avg/4, max = 4 avg)
 W = int(os.environ.get("DSX_SCANL_WAVES", "8"))
 n = int(gib * (1 << 30))
 ctx = _lib.Context(0)
@@ -26,7 +27,7 @@ t = torch.empty(n, dtype=torch.uint8, device="cuda")
 _lib.check(L.dsx_gen_uniform(ctx.h, ctypes.c_void_p(t.data_ptr()), 0, n, 1), ctx.h)
 for i in range(3):
     print(f"scan_trace: call {i}", flush=True)
-    desync_amd.cut_device(t.data_ptr(), n, 16384, 65536, 262144, ctx=ctx)
+    desync_amd.cut_device(t.data_ptr(), n, avg // 4, avg, avg * 4, ctx=ctx)
 st = ctx.stats()
 st_scan_ms, st_stitch_ms = st.scan_ms, st.stitch_ms
 print(f"stats: chunks {st.chunks} candidates {st.candidates} repaired {st.repaired_segments} "
@@ -94,3 +95,7 @@ if len(wk):
         print(f"  {name:7s} pct {q} {np.percentile(rel[:, i], q).round(1).tolist()}")
     for c, name in ((7, "seek"), (9, "chain")):
         print(f"  {name:7s} pct {q} {np.percentile((wk[:, c] - t0) / 100.0, q).round(1).tolist()}")
+    print("walk phase durations per workgroup, us")
+    for (i, j), name in (((0, 1), "counts"), ((1, 2), "staging"), ((2, 3), "phase 1"), ((3, 4), "phase 2"),
+                         ((7, 9), "1st chain")):
+        print(f"  {name:9s} pct {q} {np.percentile((wk[:, j] - wk[:, i]) / 100.0, q).round(2).tolist()}")
