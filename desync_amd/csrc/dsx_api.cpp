@@ -202,6 +202,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_SEG_MAX")) c->seg_max_mult = std::max(1, atoi(v));
   if (const char* v = getenv("DSX_SEG_TARGET")) c->seg_target = (uint64_t)std::max(0L, atol(v));
   if (const char* v = getenv("DSX_WALK_WGS")) c->walk_wgs = std::max(1, std::min(4, atoi(v)));
+  if (const char* v = getenv("DSX_WALK_NT")) c->walk_nt = atoi(v) == 576 ? 576 : 256;
   if (const char* v = getenv("DSX_DIGEST_PF")) c->digest_pf = atoi(v) != 0;
   if (const char* v = getenv("DSX_TAIL_MULT")) c->tail_mult = std::max(1, std::min(4, atoi(v)));
   if (const char* v = getenv("DSX_LANE_BYTES")) {
@@ -1003,6 +1004,8 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
   const size_t walk_lds = (size_t)kWalkLdsCap * 4 + (kMaxSpg + 1) * 8;
   if (wide)
     hipLaunchKernelGGL(walk_kernel<1024>, dim3(walk_grid), dim3(1024), walk_lds, c->stream, ta);
+  else if (c->walk_nt == 576 && spg == 8)  // (the 8 GiB pieces: 8 segments + the redundant one, a wave each)
+    hipLaunchKernelGGL(walk_kernel<576>, dim3(walk_grid), dim3(576), walk_lds, c->stream, ta);
   else
     hipLaunchKernelGGL(walk_kernel<256>, dim3(walk_grid), dim3(256), walk_lds, c->stream, ta);
   HIPCHK(c, hipGetLastError());
@@ -1050,6 +1053,9 @@ int ensure_attr_walk(dsx_ctx* c) {
   static bool done = false;
   if (!done) {
     HIPCHK(c, hipFuncSetAttribute((const void*)walk_kernel<256>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kWalkLdsCap * 4 + (kMaxSpg + 1) * 8)));
+    HIPCHK(c, hipFuncSetAttribute((const void*)walk_kernel<576>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kWalkLdsCap * 4 + (kMaxSpg + 1) * 8)));
     HIPCHK(c, hipFuncSetAttribute((const void*)walk_kernel<1024>,

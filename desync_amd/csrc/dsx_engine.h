@@ -134,6 +134,7 @@ struct dsx_ctx {
   uint64_t seg_floor = 1ull << 20;    // DSX_SEG_FLOOR
   uint64_t seg_target = 4096;         // DSX_SEG_TARGET: double the segment while a span has more (0: off)
   int walk_wgs = 2;                   // DSX_WALK_WGS: walk workgroups per CU the segments are spread over
+  int walk_nt = 576;                  // DSX_WALK_NT: 576 = one wave per chain at 8 segments per workgroup (256: 4 waves)
   bool scan_trace = false;            // DSX_SCAN_TRACE: per-wave timestamps of the last scan
   bool wave_major = true;             // DSX_WAVE_MAJOR: scanl's first regions wave-major
   int scan_nt = 1;                    // DSX_SCAN_NT: line DMA cache policy (0 none, 1 nt: default, 2 sc1, 3 sc0 sc1 nt)

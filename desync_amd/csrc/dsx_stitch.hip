@@ -137,9 +137,10 @@ __device__ uint32_t walk_block_scan(uint32_t v, uint32_t* s_wave, uint32_t* tota
   return before + incl - v;
 }
 
-// NT = 256 threads (spread over the chip), or 1024 (split streams: a few
-// workgroups beside the next piece's scan, on the CUs it leaves free, each
-// wave walking several segments)
+// NT = 576 threads for 8 segments per workgroup (an 8 GiB piece: every chain
+// its own wave, so phase 1 is one chain long), 256 otherwise, or 1024 (split
+// streams: a few workgroups beside the next piece's scan, on the CUs it leaves
+// free, each wave walking several segments)
 template <int NT>
 __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
   constexpr int kWalkThreads = NT;
@@ -287,14 +288,33 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
         // DESIGN.md 4.2)
         if (x < rc.tail_at) {
           uint64_t m = __ballot(src.v > x + rc.min);
-          while (m != 0) {  // (m == 0: window exhausted, rel_step refills)
-            const uint32_t l = (uint32_t)__builtin_ctzll(m);
-            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)src.v, (int)l);
-            if (__builtin_expect(c > min(x + rc.max, cap), 0)) break;
-            cm |= 1ull << l;
-            x = c;
-            m = __ballot(src.v > x + rc.min);
-          }
+          // while (m != 0) {  (m == 0: window exhausted, rel_step refills)
+          //   l = ctz(m); c = v[l]; if (c > min(x + max, cap)) break;
+          //   cm |= 1 << l; x = c; m = ballot(v > x + min); }
+          // by hand: the compiler's form of this loop takes 18 instructions
+          // a step (a select and a vcc copy per exit test), these 13; the
+          // steps of all the CU's walking waves share its scalar unit
+          uint32_t l, c, lim, xm;
+          asm volatile(
+              "L_walk_step_%=:\n\t"
+              "s_cmp_eq_u64 %[m], 0\n\t"
+              "s_cbranch_scc1 L_walk_out_%=\n\t"
+              "s_ff1_i32_b64 %[l], %[m]\n\t"
+              "s_add_u32 %[lim], %[x], %[mx]\n\t"
+              "v_readlane_b32 %[c], %[v], %[l]\n\t"
+              "s_min_u32 %[lim], %[lim], %[cap]\n\t"
+              "s_cmp_gt_u32 %[c], %[lim]\n\t"
+              "s_cbranch_scc1 L_walk_out_%=\n\t"
+              "s_bitset1_b64 %[cm], %[l]\n\t"
+              "s_add_u32 %[xm], %[c], %[mn]\n\t"
+              "s_mov_b32 %[x], %[c]\n\t"
+              "v_cmp_lt_u32_e64 %[m], %[xm], %[v]\n\t"
+              "s_branch L_walk_step_%=\n"
+              "L_walk_out_%=:"
+              : [m] "+s"(m), [x] "+s"(x), [cm] "+s"(cm), [l] "=&s"(l), [c] "=&s"(c),
+                [lim] "=&s"(lim), [xm] "=&s"(xm)
+              : [v] "v"(src.v), [mx] "s"(rc.max), [mn] "s"(rc.min), [cap] "s"(cap)
+              : "scc");
         }
         flush();  // (before rel_step moves the window)
         uint32_t nx;
@@ -413,6 +433,7 @@ __global__ __launch_bounds__(NT) void walk_kernel(StitchArgs a) {
 
 template __global__ void walk_kernel<256>(StitchArgs);
 template __global__ void walk_kernel<1024>(StitchArgs);
+template __global__ void walk_kernel<576>(StitchArgs);
 
 // ---- K3: validity propagation, sequential repair, scan of counts ----------
 constexpr int kFixThreads = 1024;
