@@ -57,7 +57,7 @@ EXPORTS = (
     "dsx_selftest_boundary", "dsx_gen_uniform", "dsx_gen_dedup", "dsx_chunk_ids",
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host", "dsx_copy",
     "dsx_ids_fd", "dsx_ids_host", "dsx_progress", "dsx_shard_resolve_async", "dsx_shard_collect",
-    "dsx_ctx_stream", "dsx_stamps_begin", "dsx_stamps_end",
+    "dsx_ctx_stream", "dsx_stamps_begin", "dsx_stamps_end", "dsx_host_copy",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
@@ -225,6 +225,7 @@ def lib():
             "dsx_ids_host": (i32, [vp, vp, u64, u64, vp, u64, i32, vp]),
             "dsx_stamps_begin": (i32, [vp, u64]),
             "dsx_stamps_end": (i32, [vp, vp, u64, P(u64)]),
+            "dsx_host_copy": (i32, [vp, vp, u64, i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

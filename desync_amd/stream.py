@@ -19,6 +19,7 @@ import weakref
 
 import numpy as np
 
+from . import _lib
 from .index import CaFormatExcludeNoDump, CaFormatSHA512256, ChunkArray, FormatIndex, Index
 
 
@@ -48,6 +49,23 @@ class ChunkStorage:
         self.ws = ws
         self._lock = threading.Lock()
         self._processed = set()
+
+    def _mark(self, ids):
+        """Marks the IDs not processed yet (one lock for a hand-off of chunks)
+        and returns their positions in ``ids``; a duplicate within ``ids``
+        counts once, like consecutive StoreChunk calls."""
+        proc, fresh = self._processed, []
+        with self._lock:
+            for i, cid in enumerate(ids):
+                if cid not in proc:
+                    proc.add(cid)
+                    fresh.append(i)
+        return fresh
+
+    def _unmark(self, ids):
+        with self._lock:
+            for cid in ids:
+                self._processed.discard(cid)
 
     def StoreChunk(self, chunk: Chunk):
         cid = chunk.ID()
@@ -84,6 +102,7 @@ class MemoryStore:
 _BATCH = 64  # chunks per hand-off to the store workers
 _READ_AHEAD = 256 << 20  # two of dsx_stream_ids' 128 MiB batches
 _SLAB = 8 << 20  # bytes per clone slab (a run's clone; runs are cut to this size)
+_COPY_THREADS = 4  # threads per clone (dsx_host_copy)
 
 
 class _ClonePool:
@@ -117,7 +136,9 @@ class _ClonePool:
         if slab is None:
             return memoryview(bytes(src))
         view = slab[:n]
-        np.copyto(view, np.frombuffer(src, np.uint8))  # (numpy drops the GIL for the copy)
+        if n:  # (libdsx's copy pool, without the GIL: one memcpy thread was 16 ms of 65 per 512 MiB)
+            _lib.check(_lib.lib().dsx_host_copy(view.ctypes.data, np.frombuffer(src, np.uint8).ctypes.data,
+                                                n, _COPY_THREADS))
         # the chunks' memoryviews keep `view` alive; when the last goes, the
         # slab is free again
         weakref.finalize(view, self._release, slab)
@@ -154,19 +175,30 @@ def ChunkStream(ctx, c, ws, n):
     errors = []
 
     def worker():
+        # ChunkStorage.StoreChunk per chunk, with the processed-ID marks taken
+        # for the whole hand-off under one lock (the per-chunk lock was a
+        # third of a worker's time); on a store error the chunk's mark and
+        # those of the hand-off's unstored chunks are taken back
+        has, store = ws.HasChunk, ws.StoreChunk
         while True:
             item = work.get()
             if item is None:
                 return
             s, ends, idb, mv, base = item
-            for i, e in enumerate(ends):
+            ids = [idb[j:j + 32] for j in range(0, len(idb), 32)]
+            fresh = storage._mark(ids)
+            for k, i in enumerate(fresh):
                 if errors:
+                    storage._unmark([ids[j] for j in fresh[k:]])
                     break
+                cid = ids[i]
                 try:
-                    storage.StoreChunk(Chunk(idb[32 * i:32 * i + 32], mv[s - base:e - base]))
+                    if not has(cid):
+                        store(Chunk(cid, mv[(ends[i - 1] if i else s) - base:ends[i] - base]))
                 except BaseException as ex:  # noqa: BLE001 -- re-raised by the producer
+                    storage._unmark([ids[j] for j in fresh[k:]])
                     errors.append(ex)
-                s = e
+                    break
 
     threads = [threading.Thread(target=worker, daemon=True) for _ in range(nw)]
     for t in threads:

@@ -205,6 +205,12 @@ int dsx_stream_unpop(dsx_ctx_t *ctx, uint64_t pos);
  * valid until the next buffer/commit/push/advance/flush/end on ctx). */
 int dsx_stream_window(dsx_ctx_t *ctx, const uint8_t **base, uint64_t *base_pos, uint64_t *len);
 const uint8_t *dsx_stream_chunk_id(dsx_ctx_t *ctx);
+/* The clone of a run of chunks out of the held bytes (index.go:196-200,
+ * slices.Clone of each chunk: ChunkStream clones a run at once): a host
+ * memcpy of n bytes split over up to `threads` threads of a persistent pool
+ * (<= 1: the calling thread alone).  dst and src must not overlap.  No
+ * context; no GPU. */
+int dsx_host_copy(void *dst, const void *src, uint64_t n, int threads);
 
 /* ---- multi-GPU shards (split-and-align across ranks) ------------------------
  * A blob of total length `total` is range-sharded; rank r holds

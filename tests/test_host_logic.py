@@ -3,6 +3,8 @@ import os
 import stat
 import struct
 
+import pytest
+
 from desync_amd import make
 
 
@@ -216,6 +218,106 @@ def test_clone_pool_reuses_released_slabs():
     assert bytes(kept) == src[100:200].tobytes()
     big = pool.clone(memoryview(np.zeros(stream._SLAB + 1, np.uint8)))  # larger than a slab
     assert isinstance(big.obj, bytes) and len(big) == stream._SLAB + 1
+
+
+def test_host_copy_pool():
+    """dsx_host_copy (ChunkStream's clone of a run): every size and thread
+    count copies the bytes exactly, including the ragged last part and sizes
+    below one part; overlapping ranges are refused.  Host only, no GPU."""
+    import ctypes
+
+    import numpy as np
+
+    from desync_amd import _lib, stream
+    L = _lib.lib()
+    rng = np.random.default_rng(11)
+    src = rng.integers(0, 256, (9 << 20) + 4321, dtype=np.uint8)
+    for n in (0, 1, 4095, 1 << 20, (1 << 20) + 1, (3 << 20) + 12345, src.size):
+        for threads in (0, 1, 2, 4, 16):
+            dst = np.zeros(n + 64, np.uint8)
+            assert L.dsx_host_copy(dst.ctypes.data, src.ctypes.data, n, threads) == 0
+            assert np.array_equal(dst[:n], src[:n]) and not dst[n:].any(), (n, threads)
+    buf = np.zeros(4 << 20, np.uint8)
+    assert L.dsx_host_copy(buf.ctypes.data + 4096, buf.ctypes.data, 2 << 20, 4) == _lib.DSX_E_INVAL
+    assert L.dsx_host_copy(None, ctypes.c_void_p(buf.ctypes.data), 16, 4) == _lib.DSX_E_INVAL
+    # the clone pool's copies go through it
+    pool = stream._ClonePool(1)
+    v = pool.clone(memoryview(src[:(5 << 20) + 7]))
+    assert bytes(v) == src[:(5 << 20) + 7].tobytes()
+
+
+def test_chunkstream_store_workers():
+    """ChunkStream's store workers over blocks of chunks (a stand-in chunker,
+    no GPU): an ID repeated within and across hand-offs is stored once (the
+    reference's ChunkStorage), a store that has an ID is not asked to store
+    it, the index lists every chunk in order, and a failing store raises out
+    of ChunkStream and no chunk is stored after it."""
+    import hashlib
+
+    import numpy as np
+
+    from desync_amd import stream
+
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 3 << 20, dtype=np.uint8).tobytes()
+    sizes = rng.integers(1000, 9000, 600)
+    ends = np.cumsum(sizes)
+    ends = ends[ends < len(data)].tolist() + [len(data)]
+    # IDs: every 7th chunk repeats the ID of the chunk before it
+    ids = [hashlib.sha256(str(i - (i % 7 == 0 and i > 0)).encode()).digest() for i in range(len(ends))]
+
+    class Blocks:
+        def __init__(self, per):
+            self.i, self.per = 0, per
+
+        def EnableIDs(self):
+            pass
+
+        def _next_block(self, clone, max_bytes):
+            i = self.i
+            if i >= len(ends):
+                return None
+            k = min(len(ends), i + self.per)
+            s = ends[i - 1] if i else 0
+            self.i = k
+            return s, ends[i:k], b"".join(ids[i:k]), clone(memoryview(data)[s:ends[k - 1]])
+
+        def Min(self):
+            return 1000
+
+        def Avg(self):
+            return 4000
+
+        def Max(self):
+            return 9000
+
+    class Store:
+        def __init__(self, fail_at=None, have=()):
+            self.got, self.fail_at, self.have = {}, fail_at, set(have)
+
+        def HasChunk(self, cid):
+            return cid in self.have
+
+        def StoreChunk(self, ch):
+            if self.fail_at is not None and len(self.got) == self.fail_at:
+                raise IOError("disk full")
+            assert ch.ID() not in self.got
+            self.got[ch.ID()] = bytes(ch.Data())
+
+    for per in (1, 5, 64, 200):
+        st = Store(have=ids[10:12])
+        idx = stream.ChunkStream(None, Blocks(per), st, 3)
+        assert [c.Start + c.Size for c in idx.Chunks] == ends
+        assert [c.ID for c in idx.Chunks] == ids
+        want = {}
+        for i, e in enumerate(ends):
+            if ids[i] not in ids[10:12]:
+                want.setdefault(ids[i], data[(ends[i - 1] if i else 0):e])
+        assert st.got == want, per
+    st = Store(fail_at=40)
+    with pytest.raises(IOError, match="disk full"):
+        stream.ChunkStream(None, Blocks(64), st, 2)
+    assert len(st.got) == 40
 
 
 def test_chunk_array_start():

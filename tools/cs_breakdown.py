@@ -82,6 +82,25 @@ def main():
         ch.close()
         return k
 
+    def blocks_nocopy():  # the same without the clone: views dropped at once (measures the copy)
+        ch = desync_amd.NewChunker(io.BytesIO(data), MIN, AVG, MAX)
+        ch.EnableIDs()
+        ch._ra = 256 << 20
+        k = 0
+        while True:
+            blk = ch._next_block(lambda v: v, 8 << 20)
+            if blk is None:
+                break
+            k += len(blk[1])
+        ch.close()
+        return k
+
+    def read_only():  # the reader alone: BytesIO.readinto in 8 MiB pieces
+        r, buf, k = io.BytesIO(data), bytearray(8 << 20), 0
+        while r.readinto(buf):
+            k += 1
+        return k
+
     from desync_amd import _lib
     shared = _lib.Context(0)
 
@@ -93,7 +112,8 @@ def main():
 
     res = {"tool": "cs_breakdown", "mib": mib}
     for name, fn in (("next", lambda: next_only(False)), ("next_ids", lambda: next_only(True)),
-                     ("producer", producer_only), ("blocks", blocks_only), ("chunkstream_1", lambda: cs(1)),
+                     ("producer", producer_only), ("blocks", blocks_only), ("blocks_nocopy", blocks_nocopy),
+                     ("read_only", read_only), ("chunkstream_1", lambda: cs(1)),
                      ("chunkstream_4", lambda: cs(4)),
                      ("cs4_shared", lambda: cs(4, shared))):
         fn()  # warm-up
