@@ -211,6 +211,45 @@ __device__ __forceinline__ bool mode2_exact(uint32_t t, const TestConsts& tc) {
   return t < tc.vmax && v - tc.qbias <= tc.qmax;
 }
 
+// Bit q of the result = (x[q] <= lim), x[0] in bit 0: a compare into a mask
+// and one v_addc (bits = 2 bits + carry, the carry-out back into that mask)
+// per value, last value first.  VCC and one SGPR pair in turn, each read at
+// least two instructions after its write (a VALU write of an SGPR read by a
+// VOP3 needs two wait states on gfx950); lim in a VGPR, so the scan's scarce
+// SGPRs are not spilled for it.  The compiler's select + or form costs a
+// v_cndmask, half a v_or3 and the same nops per value.
+__device__ __forceinline__ uint32_t le_bits8(const uint32_t (&x)[8], uint32_t lim_v) {
+  uint32_t b;
+  uint64_t m;
+  asm volatile(
+      "v_cmp_ge_u32_e64 vcc, %[lim], %[x7]\n\t"
+      "v_cmp_ge_u32_e64 %[m], %[lim], %[x6]\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e64 %[b], vcc, 0, 0, vcc\n\t"
+      "v_cmp_ge_u32_e64 vcc, %[lim], %[x5]\n\t"
+      "v_addc_co_u32_e64 %[b], %[m], %[b], %[b], %[m]\n\t"
+      "v_cmp_ge_u32_e64 %[m], %[lim], %[x4]\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e64 %[b], vcc, %[b], %[b], vcc\n\t"
+      "v_cmp_ge_u32_e64 vcc, %[lim], %[x3]\n\t"
+      "v_addc_co_u32_e64 %[b], %[m], %[b], %[b], %[m]\n\t"
+      "v_cmp_ge_u32_e64 %[m], %[lim], %[x2]\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e64 %[b], vcc, %[b], %[b], vcc\n\t"
+      "v_cmp_ge_u32_e64 vcc, %[lim], %[x1]\n\t"
+      "v_addc_co_u32_e64 %[b], %[m], %[b], %[b], %[m]\n\t"
+      "v_cmp_ge_u32_e64 %[m], %[lim], %[x0]\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e64 %[b], vcc, %[b], %[b], vcc\n\t"
+      "s_nop 0\n\t"
+      "v_addc_co_u32_e64 %[b], %[m], %[b], %[b], %[m]"
+      : [b] "=&v"(b), [m] "=&s"(m)
+      : [lim] "v"(lim_v), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]),
+        [x4] "v"(x[4]), [x5] "v"(x[5]), [x6] "v"(x[6]), [x7] "v"(x[7])
+      : "vcc");
+  return b;
+}
+
 template <int MODE>
 __device__ __forceinline__ bool is_cand(uint32_t h, const TestConsts& tc) {
   if constexpr (MODE == 2) {
@@ -772,6 +811,11 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
   TestConsts tcv = a.tc;
   asm volatile("" : "+v"(tcv.c0));
   asm volatile("" : "+v"(tcv.madc));
+  // the rare path's constants (le_bits8), in VGPRs: the kernel has no SGPRs
+  // to spare and spills whatever it keeps in them across the loop
+  uint32_t qlim_v = tcv.qmax + tcv.qbias, rot_v = tcv.rot;
+  asm volatile("" : "+v"(qlim_v));
+  asm volatile("" : "+v"(rot_v));
 
   // Region r's descriptor starts at its warm-up line (grid-relative
   // r*RB - 128), shifted by shift0 for region 0 so it never precedes the
@@ -1128,7 +1172,20 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
         }
         if (__builtin_expect(__ballot(mn < thr) != 0, 0)) {
           uint32_t bits = 0;
-          if (MODE == 2 && tcv.rot == 0) {
+          if (MODE == 2 && VARIANT == 0 && __builtin_expect(__ballot(mn == 0u) == 0, 1)) {
+            // no t == 0 in the wave (t = 0 is h = 2^32 - 1, 2^-32 a byte):
+            // then x - qBias <= qMax is x <= qMax + qBias, with x = t (odd d)
+            // or rotl(t, -k) (even d), both >= 1, so qBias in {0, 1} cannot
+            // wrap -- one compare and one add-carry per byte
+            if (tcv.rot == 0) {
+              bits = le_bits8(t, qlim_v);
+            } else {
+              uint32_t x[8];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) x[q] = __builtin_amdgcn_alignbit(t[q], t[q], rot_v);
+              bits = le_bits8(x, qlim_v);
+            }
+          } else if (MODE == 2 && tcv.rot == 0) {
             // odd d (k = 0, the default parameters): t = (h+1)*inv here, and
             // chunker.go:265's test is t - qBias <= qMax with no rotate
 #pragma unroll

@@ -5,7 +5,8 @@
 #   under rocprofv3 --kernel-trace --stats; an L2 read-request --pmc pass (HBM
 #   bytes per launch) and a GRBM_GUI_ACTIVE / SQ_BUSY_CYCLES pass; the dedup
 #   and zeros workloads; chunk-ID, IndexFromFile / VerifyIndex and streaming
-#   rates.  tools/profile_summary.py condenses it into SUMMARY.txt.
+#   rates; the --avg 16 / 64 / 256 sweep (tools/ab.py, alternating processes).
+#   tools/profile_summary.py condenses it into SUMMARY.txt.
 #   tools/round_profile.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
@@ -35,6 +36,8 @@ done
 timeout -k 10 400 python3 tools/digest_rate.py 1 4 16 > $OUT/digest_rate.json 2> $OUT/digest_rate.err || { tail $OUT/digest_rate.err; exit 1; }
 timeout -k 10 600 python3 tools/make_rate.py 1 4 > $OUT/make_rate.json 2> $OUT/make_rate.err || { tail $OUT/make_rate.err; exit 1; }
 timeout -k 10 300 python3 tools/stream_rate.py > $OUT/stream_rate.json 2> $OUT/stream_rate.err || { tail $OUT/stream_rate.err; exit 1; }
+timeout -k 10 600 python3 tools/ab.py --rounds 3 $OUT/avg 'a16:+--avg=16' 'a64:+--avg=64' 'a256:+--avg=256' > $OUT/avg_sweep.txt 2>&1 || { tail $OUT/avg_sweep.txt; exit 1; }
+grep "^==" $OUT/avg_sweep.txt
 python3 -c "
 import json
 for r in json.load(open('$OUT/digest_rate.json'))['rows']: print('ids', r['gib'], {k: v for k, v in r.items() if k.endswith('_gibs')})
