@@ -295,6 +295,44 @@ def test_periodic_dense_candidates(dctx):
     assert np.array_equal(gpu_cut(dctx, data), o.chunk_stream(data, MIN, AVG, MAX))
 
 
+def _window_with_hash(target, seed):
+    """A 48-byte window whose rolling hash (chunker.go:225-228) is `target`:
+    44 random bytes, the last 4 by meet-in-the-middle over two byte pairs."""
+    rng = np.random.default_rng(seed)
+    T = np.array([int(v) for v in o.T], dtype=np.uint64)
+    rot = lambda v, r: ((v << np.uint64(r)) | (v >> np.uint64(32 - r))) & np.uint64(0xFFFFFFFF) if r else v
+    while True:
+        w = rng.integers(0, 256, 48, dtype=np.uint8)
+        w[44:] = 0
+        resid = np.uint64(target ^ o.window_hash(bytes(w)) ^ int(rot(T[0], 3) ^ rot(T[0], 2) ^ rot(T[0], 1) ^ T[0]))
+        a = (rot(T, 3)[:, None] ^ rot(T, 2)[None, :]).ravel()           # bytes 44, 45
+        b = (rot(T, 1)[:, None] ^ T[None, :] ^ resid).ravel()           # bytes 46, 47
+        common, ia, ib = np.intersect1d(a, b, return_indices=True)
+        if common.size:
+            w[44], w[45] = divmod(int(ia[0]), 256)
+            w[46], w[47] = divmod(int(ib[0]), 256)
+            assert o.window_hash(bytes(w)) == target
+            return w
+
+
+@pytest.mark.parametrize("avg", [16 * 1024, 64 * 1024, 256 * 1024])
+def test_scan_hash_all_ones(dctx, avg):
+    """Windows whose hash is 2^32 - 1, where the boundary test's product
+    (h+1)*inv is 0: the scan's hit path bounds x - qBias <= qMax as
+    x <= qMax + qBias only for waves with no such product, and a wave with one
+    takes the exact form.  The window is planted 200 times (next to real
+    candidates too) at odd and even d; the cuts must equal the oracle's."""
+    w = _window_with_hash(0xFFFFFFFF, 9)
+    mn, mx = avg // 4, avg * 4
+    data = o.synth_uniform(41, 0, 12 << 20).copy()
+    cands = o.candidates(data, mn, avg, mx)
+    rng = np.random.default_rng(2)
+    spots = list(rng.integers(0, data.size - 48, 150)) + [int(c) - 60 for c in cands[:50] if c > 60]
+    for s in spots:
+        data[s:s + 48] = w
+    assert np.array_equal(gpu_cut(dctx, data, mn, avg, mx), o.chunk_stream(data, mn, avg, mx))
+
+
 def test_stitch_many_workgroups_and_repairs(monkeypatch):
     """The stitch on many walk workgroups (small segments) and on seams inside
     zero runs (suspect segments: fixup_kernel's sequential repair)."""
