@@ -7,6 +7,7 @@
 #include <array>
 #include <atomic>
 #include <deque>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -358,6 +359,9 @@ int read_state(dsx_ctx* c, HostState* out);
 int enqueue_piece(dsx_ctx* c, const CallCfg& cc, const uint8_t* d_piece, uint64_t halo,
                   uint64_t P, uint64_t len, bool is_last);
 int ensure_attr_walk(dsx_ctx* c);
+// host threads (dsx_stream.cpp): fn(0) on the caller, fn(1..parts-1) on a
+// persistent pool; returns when all have returned
+void host_parallel(int parts, const std::function<void(int)>& fn);
 // launch the stitch tasks of the queued calls still behind (before any other
 // work on the context, and when such a call is collected)
 int flush_behind(dsx_ctx* c);

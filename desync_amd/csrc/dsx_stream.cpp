@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -603,35 +604,29 @@ extern "C" int dsx_stream_advance(dsx_ctx_t* c, uint64_t n) {
   return DSX_OK;
 }
 
-// ---- dsx_host_copy: ChunkStream's clone of a run (index.go:196-200) -------
-// One memcpy thread moves ~15 GB/s out of the pinned buffer: 512 MiB of
-// clones were 16 ms of ChunkStream's 65 (profiles/r05v/cs.json).  The pool's
-// threads persist (a thread per call would cost more than a slab's copy);
-// they are detached and the pool is never destroyed, so process exit does not
-// wait on them.
+// ---- host_parallel: a persistent pool of host threads ----------------------
+// One job at a time: fn(0) on the calling thread, fn(1..parts-1) on pool
+// threads.  The threads persist (one per call would cost more than a
+// ChunkStream slab's copy); they are detached and the pool is never
+// destroyed, so process exit does not wait on them.
 namespace {
-class CopyPool {
+class HostPool {
  public:
-  void run(uint8_t* d, const uint8_t* s, uint64_t n, int parts) {
-    std::lock_guard<std::mutex> call(call_mu_);  // one copy at a time through the pool
+  void run(int parts, const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> call(call_mu_);  // one job at a time through the pool
     while ((int)threads_ < parts - 1) {
       const int idx = ++threads_;
       std::thread([this, idx] { loop(idx); }).detach();
     }
-    const uint64_t step = ((n + parts - 1) / parts + 4095) & ~uint64_t(4095);
     {
       std::lock_guard<std::mutex> g(mu_);
-      d_ = d;
-      s_ = s;
-      n_ = n;
-      step_ = step;
+      fn_ = &fn;
       parts_ = parts;
-      pending_ = 0;
-      for (int i = 1; i < parts; ++i) pending_ += (uint64_t)i * step < n ? 1 : 0;
+      pending_ = parts - 1;
       ++gen_;
     }
     cv_.notify_all();
-    memcpy(d, s, std::min(step, n));  // part 0 on the calling thread
+    fn(0);
     std::unique_lock<std::mutex> g(mu_);
     done_.wait(g, [&] { return pending_ == 0; });
   }
@@ -643,27 +638,34 @@ class CopyPool {
     for (;;) {
       cv_.wait(g, [&] { return gen_ != seen; });
       seen = gen_;
-      const uint64_t off = (uint64_t)idx * step_;
-      if (idx >= parts_ || off >= n_) continue;  // (no part for this thread in this copy)
-      uint8_t* d = d_ + off;
-      const uint8_t* s = s_ + off;
-      const uint64_t len = std::min(step_, n_ - off);
+      if (idx >= parts_) continue;  // (no part for this thread in this job)
+      const std::function<void(int)>* fn = fn_;
       g.unlock();
-      memcpy(d, s, len);
+      (*fn)(idx);
       g.lock();
       if (--pending_ == 0) done_.notify_one();
     }
   }
   std::mutex call_mu_, mu_;
   std::condition_variable cv_, done_;
-  int threads_ = 0;
-  uint8_t* d_ = nullptr;
-  const uint8_t* s_ = nullptr;
-  uint64_t n_ = 0, step_ = 0, gen_ = 0, pending_ = 0;
-  int parts_ = 0;
+  int threads_ = 0, parts_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  const std::function<void(int)>* fn_ = nullptr;
 };
 }  // namespace
 
+void host_parallel(int parts, const std::function<void(int)>& fn) {
+  if (parts <= 1) {
+    fn(0);
+    return;
+  }
+  static HostPool* pool = new HostPool;  // (never destroyed: detached threads wait on it)
+  pool->run(std::min(parts, 64), fn);
+}
+
+// ---- dsx_host_copy: ChunkStream's clone of a run (index.go:196-200) -------
+// One memcpy thread moves ~15 GB/s out of the pinned buffer: 512 MiB of
+// clones were 16 ms of ChunkStream's 65 (profiles/r05v/cs.json).
 extern "C" int dsx_host_copy(void* dst, const void* src, uint64_t n, int threads) {
   if (n && (!dst || !src)) return DSX_E_INVAL;
   const uint8_t* s = (const uint8_t*)src;
@@ -674,7 +676,10 @@ extern "C" int dsx_host_copy(void* dst, const void* src, uint64_t n, int threads
     if (n) memcpy(d, s, n);
     return DSX_OK;
   }
-  static CopyPool* pool = new CopyPool;  // (never destroyed: detached threads wait on it)
-  pool->run(d, s, n, parts);
+  const uint64_t step = ((n + parts - 1) / parts + 4095) & ~uint64_t(4095);
+  host_parallel(parts, [&](int i) {
+    const uint64_t off = (uint64_t)i * step;
+    if (off < n) memcpy(d + off, s + off, std::min(step, n - off));
+  });
   return DSX_OK;
 }
