@@ -117,10 +117,10 @@ int dsx_progress(dsx_ctx_t *ctx, uint64_t *bytes);
  * the blob inside dsx_result().  If cap is too small the call returns
  * DSX_E_CAPACITY and *n_out holds the required count (an upper bound of
  * len/min + 2 always suffices).  A queued call's stitch publishes its state
- * into pinned host memory and dsx_result() polls it (no event per call);
- * with the environment variable DSX_FUSE=1 (off by default) the stitch of a
- * queued one-piece call runs as tasks inside the next queued calls' scans
- * and is completed by dsx_result() when no later call carries it. */
+ * into pinned host memory and dsx_result() polls it (no event per call).
+ * (The diagnostic build libdsx_diag.so also has DSX_FUSE=1: the stitch of a
+ * queued one-piece call as tasks inside the next queued calls' scans; the
+ * product library does not read it, INTEGRATION.md "Environment".) */
 int dsx_cut_device(dsx_ctx_t *ctx, const void *d_blob, uint64_t len, const dsx_params_t *p,
                    uint64_t *out_ends, uint64_t cap, uint64_t *n_out, uint32_t flags);
 int dsx_sync(dsx_ctx_t *ctx);
@@ -311,7 +311,8 @@ int dsx_selftest_boundary(dsx_ctx_t *ctx, const dsx_params_t *p, int mode, uint6
                           uint64_t n, uint64_t *mismatches);
 
 /* Timeline of the last piece when the context was created with
- * DSX_SCAN_TRACE=1 (s_memrealtime ticks, 100 MHz): *n_scan wave-slot records
+ * DSX_SCAN_TRACE=1 (libdsx_diag.so only; the product library records none and
+ * returns zero records) (s_memrealtime ticks, 100 MHz): *n_scan wave-slot records
  * {start, end, regions} of the line-aligned scan, then *n_walk stitch-walk
  * workgroup records {entry, counts scanned, candidates staged, speculative
  * walks done, staged walks done, s_memtime at staged, s_memtime at
