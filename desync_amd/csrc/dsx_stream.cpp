@@ -419,9 +419,13 @@ extern "C" int dsx_stream_pop(dsx_ctx_t* c, uint64_t* start, uint64_t* size) {
     if (!s.fly.empty()) {
       // collect now if the oldest batch is finished, if no more input can
       // come, or if enough batches are queued; otherwise ask for input
-      // first, so the reader works while the GPU does
+      // first, so the reader works while the GPU does.  With IDs every slot
+      // may fill first: the first batch's IDs take ~15 ms (its longest
+      // chunk's SHA chain), which the reader spends reading the next batch
+      // instead of waiting (ChunkStream)
       const bool ready = hipEventQuery(s.done_ev[s.fly.front().slot]) == hipSuccess;
-      if (!(ready || s.eof || s.fly.size() >= 2)) break;
+      const size_t enough = s.ids >= 0 ? (size_t)kSlots : 2;
+      if (!(ready || s.eof || s.fly.size() >= enough)) break;
       HIPCHK(c, hipSetDevice(c->device));
       int rc = st_collect(c);
       if (!rc) rc = st_pump(c, false);  // (re-issues after a dense redo)
