@@ -82,6 +82,7 @@ class Stats(ctypes.Structure):
         ("scan_ms", ctypes.c_float), ("stitch_ms", ctypes.c_float),
         ("chunks_discarded", ctypes.c_uint64),
         ("device_bytes", ctypes.c_uint64),
+        ("host_tail_chunks", ctypes.c_uint64),
     ]
 
 
@@ -142,7 +143,7 @@ def _share_torch_hip_runtime():
 # "Environment"; tests/test_abi.py checks the library's strings against it).
 PRODUCT_ENV = ("DSX_TAIL_SPLIT", "DSX_LANE_TARGET", "DSX_SEG_FLOOR", "DSX_SCAN_NT",
                "DSX_DIGEST_PC", "DSX_DIGEST_LPT", "DSX_INDEX_WINDOW", "DSX_INDEX_SLOT",
-               "DSX_INDEX_READERS")
+               "DSX_INDEX_READERS", "DSX_INDEX_HOST_TAIL")
 # Settings only libdsx_diag.so reads (scan ablations, other geometries,
 # rejected experiments), with the value the product library behaves as (None:
 # no such value).  Set to anything else with the product library they would

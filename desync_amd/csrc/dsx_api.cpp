@@ -181,6 +181,7 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_INDEX_WINDOW")) c->index_window = (uint64_t)std::max(1L << 16, atol(v));
   if (const char* v = getenv("DSX_INDEX_SLOT")) c->index_slot = (uint64_t)std::max(1L << 12, atol(v));
   if (const char* v = getenv("DSX_INDEX_READERS")) c->index_readers = std::max(1, std::min(32, atoi(v)));
+  if (const char* v = getenv("DSX_INDEX_HOST_TAIL")) c->index_host_tail = std::max(-1L, atol(v));
 #if DSX_DIAG
   // ablation variants, alternative geometries and rejected experiments
   if (const char* m = getenv("DSX_TEST_MODE")) c->force_mode = atoi(m);

@@ -28,6 +28,9 @@ struct DigestArgs {
   // longest-first queue order (digest_order_*_kernel): queue position k takes
   // chunk order[k]; null: index order
   const uint32_t* order;
+  // chunks longer than this get no ID here (0: none): the index pipeline
+  // hashes them on the host (dsx_index.cpp, host tail)
+  uint64_t skip_above;
 };
 
 // Longest-first order of a digest range (LPT): a counting sort of the chunks

@@ -581,6 +581,10 @@ __global__ __launch_bounds__(kDigestThreads) void digest_kernel(DigestArgs a) {
     while (k < n) {
       ci = a.order ? (uint64_t)a.order[k] : k;
       const uint64_t sa = ci == 0 ? first_start : ends[ci - 1], ea = ends[ci];
+      if (a.skip_above && sa <= ea && ea - sa > a.skip_above) {  // hashed on the host
+        k = (uint64_t)nfirst + atomicAdd(a.queue, 1u);
+        continue;
+      }
       // a chunk outside the readable bytes (malformed ends) is skipped and
       // gets no ID instead of reading out of bounds
       if (sa >= a.base_off && sa <= ea && ea - a.base_off <= a.len) {
@@ -715,6 +719,10 @@ __global__ __launch_bounds__(128, 1) void digest_pc_kernel(DigestArgs a) {
   auto start_chunk = [&]() {
     while (ci < n) {
       const uint64_t sa = ci == 0 ? first_start : ends[ci - 1], ea = ends[ci];
+      if (a.skip_above && sa <= ea && ea - sa > a.skip_above) {  // hashed on the host
+        ci = (uint64_t)nfirst + atomicAdd(a.queue, 1u);
+        continue;
+      }
       if (sa >= a.base_off && sa <= ea && ea - a.base_off <= a.len) {
         s = sa - a.base_off;
         e = ea - a.base_off;

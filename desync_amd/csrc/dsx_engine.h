@@ -303,6 +303,7 @@ struct dsx_ctx {
   uint64_t index_window = 1ull << 30;  // DSX_INDEX_WINDOW: bytes per HBM window
   uint64_t index_slot = 32ull << 20;   // DSX_INDEX_SLOT: bytes per pinned read slot
   int index_readers = 4;               // DSX_INDEX_READERS: reader threads
+  int64_t index_host_tail = -1;       // DSX_INDEX_HOST_TAIL: -1 auto, 0 off, > 0 chunks longer than this on the host
   uint8_t* idx_slots[kIdxSlots] = {};
   uint64_t idx_slot_bytes = 0;
   DevBuf<uint8_t> idx_win[2];
@@ -362,6 +363,11 @@ int ensure_attr_walk(dsx_ctx* c);
 // host threads (dsx_stream.cpp): fn(0) on the caller, fn(1..parts-1) on a
 // persistent pool; returns when all have returned
 void host_parallel(int parts, const std::function<void(int)>& fn);
+// SHA-512/256 on the host (dsx_hostsha.cpp): one message, or 8 at once in
+// AVX-512 lanes (only when host_sha_vec(); n[i] == UINT64_MAX: unused lane)
+bool host_sha_vec();
+void host_sha512_256_one(const uint8_t* p, uint64_t n, uint8_t* out);
+void host_sha512_256_x8(const uint8_t* const p[8], const uint64_t n[8], uint8_t* const out[8]);
 // launch the stitch tasks of the queued calls still behind (before any other
 // work on the context, and when such a call is collected)
 int flush_behind(dsx_ctx* c);

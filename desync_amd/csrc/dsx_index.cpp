@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <condition_variable>
 #include <cstring>
@@ -186,6 +187,108 @@ struct ProgressScope {
   void set(uint64_t v) { c->prog_done.store(v); }
 };
 
+// ---- host tail --------------------------
+// The last window's digest starts when the read ends and lasts its longest
+// chunk's SHA chain: ~38 ns per byte on one GPU lane, ~10 ms for 256 KiB.
+// The longest chunks of that window go to the host instead (AVX-512, 8 per
+// core at once), the GPU skipping them (DigestArgs.skip_above): the cut L is
+// where the host's bytes over its threads take as long as the GPU's longest
+// remaining chain.
+constexpr double kGpuNsPerByte = 38.0;   // digest_pc_kernel, one lane
+constexpr double kHostNsPerByte = 1.0;   // one host thread, read + hash (AVX-512)
+constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
+constexpr int kTailThreads = 16;
+
+struct TailChunk {
+  uint64_t idx, start, len;
+};
+
+// The chunks of ranges [i0, i1) (ends e, the first starting at first) that the
+// host hashes, longest first; empty: none.  *cut = the GPU's skip_above.
+std::vector<TailChunk> plan_tail(const dsx_ctx* c, const std::vector<uint64_t>& e, uint64_t i0,
+                                 uint64_t first, int threads, uint64_t* cut) {
+  std::vector<TailChunk> t(e.size());
+  for (size_t i = 0; i < e.size(); ++i) {
+    const uint64_t s = i ? e[i - 1] : first;
+    t[i] = {i0 + i, s, e[i] - s};
+  }
+  std::sort(t.begin(), t.end(), [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
+  *cut = 0;
+  if (t.empty()) return {};
+  size_t k = 0;
+  if (c->index_host_tail > 0) {  // forced cut (tests)
+    while (k < t.size() && t[k].len > (uint64_t)c->index_host_tail) ++k;
+    *cut = (uint64_t)c->index_host_tail;
+  } else {
+    // k chunks to the host: time max(host bytes / threads, GPU's longest chain)
+    const double now = kGpuNsPerByte * (double)t[0].len;
+    double best = now, bytes = 0;
+    for (size_t j = 0; j + 1 < t.size(); ++j) {
+      bytes += (double)t[j].len;
+      const double tj = std::max(bytes * kHostNsPerByte / threads, kGpuNsPerByte * (double)t[j + 1].len);
+      if (tj < best) {
+        best = tj;
+        k = j + 1;
+      }
+      if (bytes * kHostNsPerByte / threads > now) break;
+    }
+    if (now - best < kTailMinGainNs) k = 0;
+    // (chunks as long as the first one left to the GPU stay there)
+    while (k > 0 && t[k - 1].len == t[k].len) --k;
+    if (k) *cut = t[k].len;
+  }
+  t.resize(k);
+  return t;
+}
+
+// Hashes the planned chunks (their bytes read again through `fill`) into
+// ids[32 j] for t[j]; 8 at a time per thread.
+int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* ids, int threads) {
+  const bool vec = host_sha_vec();
+  const uint64_t per = vec ? 8 : 1;
+  const uint64_t groups = (t.size() + per - 1) / per;
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> err{DSX_OK};
+  host_parallel((int)std::min<uint64_t>((uint64_t)threads, groups), [&](int) {
+    std::vector<uint8_t> buf;
+    for (uint64_t g; err.load() == DSX_OK && (g = next.fetch_add(1)) < groups;) {
+      const uint64_t j0 = g * per, j1 = std::min<uint64_t>(t.size(), j0 + per);
+      uint64_t total = 0;
+      for (uint64_t j = j0; j < j1; ++j) total += t[j].len;
+      if (buf.size() < total + 1) buf.resize(total + 1);
+      const uint8_t* p[8];
+      uint64_t n[8];
+      uint8_t* o[8];
+      uint64_t at = 0;
+      for (uint64_t j = j0; j < j0 + per; ++j) {
+        const int q = (int)(j - j0);
+        if (j >= j1) {
+          p[q] = nullptr;
+          n[q] = UINT64_MAX;
+          o[q] = nullptr;
+          continue;
+        }
+        if (t[j].len) {
+          const int rc = fill(ud, buf.data() + at, t[j].start, t[j].len);
+          if (rc) {
+            err.store(rc);
+            return;
+          }
+        }
+        p[q] = buf.data() + at;
+        n[q] = t[j].len;
+        o[q] = ids + 32 * j;
+        at += t[j].len;
+      }
+      if (vec)
+        host_sha512_256_x8(p, n, o);
+      else
+        host_sha512_256_one(p[0], n[0], o[0]);
+    }
+  });
+  return err.load();
+}
+
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
               uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {
   HIPCHK(c, hipSetDevice(c->device));
@@ -193,6 +296,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   int rc = ensure_attr_walk(c);
   if (rc) return rc;
   *n_out = 0;
+  c->stats.host_tail_chunks = 0;
   if (len == 0) return DSX_OK;  // empty file: no chunks (TestChunkerEmptyFile)
   const uint64_t need = len / p->min + 2;
   // geometry: pieces (pinned slots) tile the windows exactly; a window keeps
@@ -254,6 +358,11 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       prog.set(n ? out_ends[n - 1] : 0);
       return err;
     };
+    // the host tail of the last window (SHA-512/256 only; auto needs AVX-512)
+    const bool tail_on = algo == DSX_DIGEST_SHA512_256 && out_ids &&
+                         (c->index_host_tail > 0 || (c->index_host_tail < 0 && host_sha_vec()));
+    std::vector<TailChunk> tail;
+    std::vector<uint8_t> tail_ids;
     for (w = 0; w < nwin; ++w) {
       ws = w * W;
       wl = std::min(W, len - ws);
@@ -308,8 +417,31 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       da.ids = c->dg_ids.p;
       da.range_lo = c->idx_snap.p + 2 * w;
       da.range_hi = c->idx_snap.p + 2 * (w + 1);
-      rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
-      if (rc) return drain(c, pf, rc);
+      if (tail_on && w + 1 == nwin) {
+        // the window's chunk ends (the stitch is done once the stream is)
+        uint64_t snap[4];
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess)
+          e = hipMemcpy(snap, c->idx_snap.p + 2 * w, sizeof snap, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: tail range"));
+        const uint64_t i0 = snap[0], i1 = std::max(snap[0], snap[2]);
+        std::vector<uint64_t> ends(i1 - i0);
+        if (i1 > i0)
+          e = hipMemcpy(ends.data(), c->out.p + i0, (i1 - i0) * 8, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: tail ends"));
+        const int threads = (int)std::max(1u, std::min<unsigned>(kTailThreads, std::thread::hardware_concurrency()));
+        tail = plan_tail(c, ends, i0, snap[1], threads, &da.skip_above);
+        rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
+        if (rc) return drain(c, pf, rc);
+        // the host's share while the GPU hashes the rest
+        tail_ids.assign(32 * tail.size(), 0);
+        if (!tail.empty()) rc = hash_tail(fill, ud, tail, tail_ids.data(), threads);
+        if (rc) return drain(c, pf, rc);
+        c->stats.host_tail_chunks = tail.size();
+      } else {
+        rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
+        if (rc) return drain(c, pf, rc);
+      }
       hipError_t e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
       if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
     }
@@ -334,6 +466,8 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     if (st.total) {
       HIPCHK(c, hipMemcpy(out_ends, c->out.p, st.total * 8, hipMemcpyDeviceToHost));
       if (out_ids) HIPCHK(c, hipMemcpy(out_ids, c->dg_ids.p, st.total * 32, hipMemcpyDeviceToHost));
+      for (size_t j = 0; j < tail.size(); ++j)  // (the GPU skipped these)
+        if (tail[j].idx < st.total) memcpy(out_ids + 32 * tail[j].idx, tail_ids.data() + 32 * j, 32);
     }
     prog.set(len);
     return DSX_OK;

@@ -416,6 +416,8 @@ typedef struct dsx_stats {
                                    discarded overlap chunks too) */
     uint64_t device_bytes;      /* HBM the context holds now (its pipeline buffers; filled in by
                                    dsx_get_stats; the caller's blob and cut list are not counted) */
+    uint64_t host_tail_chunks;  /* dsx_index_*: chunks of the last window hashed on the host
+                                   (DSX_INDEX_HOST_TAIL) while the GPU hashed the others */
 } dsx_stats_t;
 int dsx_get_stats(dsx_ctx_t *ctx, dsx_stats_t *out);
 

@@ -102,6 +102,47 @@ def test_index_fd_reader_threads(tmp_path, monkeypatch, readers):
     assert [bytes(x) for x in ids] == _ids(data, ref, "sha512-256")
 
 
+@pytest.mark.parametrize("tail", ["65536", "0", "-1"])
+def test_index_host_tail(tmp_path, monkeypatch, tail):
+    """DSX_INDEX_HOST_TAIL (make.go:223's Digest.Sum for the last window's
+    longest chunks on the host, AVX-512 multi-buffer SHA-512/256, while the
+    GPU digest skips them): forced for every chunk above 64 KiB, off, and the
+    default (the pipeline's own cut).  Several windows, so only the last one
+    has a tail; from a file and from host memory.  The cut list equals the
+    oracle's and every ID hashlib's; the stats count the host's chunks."""
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_INDEX_HOST_TAIL", tail)
+    monkeypatch.setenv("DSX_INDEX_WINDOW", str(16 << 20))
+    data = o.synth_uniform(47, 0, (40 << 20) + 777)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    want = _ids(data, ref, "sha512-256")
+    long_chunks = int(np.sum(np.diff(np.concatenate([[0], ref.astype(np.int64)])) > 65536))
+    ctx = _lib.Context(0)
+    try:
+        fd = os.open(str(f), os.O_RDONLY)
+        try:
+            ends, ids = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+        finally:
+            os.close(fd)
+        n_host = ctx.stats().host_tail_chunks
+        assert np.array_equal(ends, ref)
+        assert [bytes(x) for x in ids] == want
+        ends2, ids2 = desync_amd.index_host(data, MIN, AVG, MAX, ctx=ctx)
+        assert np.array_equal(ends2, ref) and [bytes(x) for x in ids2] == want
+        assert ctx.stats().host_tail_chunks == n_host
+    finally:
+        ctx.close()
+    if tail == "0":
+        assert n_host == 0
+    elif tail == "65536":
+        assert 0 < n_host < long_chunks  # (the last window's share of them)
+    else:
+        assert n_host < long_chunks
+
+
 def test_index_host_two_gib_windows():
     """1.5 GiB through the default 1 GiB windows (two of them): every cut
     against oracle.chunk_parallel, every ID against hashlib."""
