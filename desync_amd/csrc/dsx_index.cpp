@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cerrno>
 #include <condition_variable>
 #include <cstring>
@@ -194,8 +196,11 @@ struct ProgressScope {
 // core at once), the GPU skipping them (DigestArgs.skip_above): the cut L is
 // where the host's bytes over its threads take as long as the GPU's longest
 // remaining chain.
-constexpr double kGpuNsPerByte = 38.0;   // digest_pc_kernel, one lane
-constexpr double kHostNsPerByte = 1.0;   // one host thread, read + hash (AVX-512)
+// (measured at the end of a 1 GiB file call, profiles/r05ao: the GPU's chain
+// runs at the clock an idle-ish GPU has then, ~58 ns per byte, against ~38 ns
+// on a busy one; 16 host threads read and hash ~43 GB/s)
+constexpr double kGpuNsPerByte = 58.0;   // digest_pc_kernel, one lane, end of a file call
+constexpr double kHostNsPerByte = 0.38;  // one host thread, read + hash (AVX-512)
 constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
 constexpr int kTailThreads = 16;
 
@@ -435,9 +440,23 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         if (rc) return drain(c, pf, rc);
         // the host's share while the GPU hashes the rest
         tail_ids.assign(32 * tail.size(), 0);
+#if DSX_DIAG
+        const auto th0 = std::chrono::steady_clock::now();
+#endif
         if (!tail.empty()) rc = hash_tail(fill, ud, tail, tail_ids.data(), threads);
         if (rc) return drain(c, pf, rc);
         c->stats.host_tail_chunks = tail.size();
+#if DSX_DIAG
+        if (getenv("DSX_TAIL_LOG")) {
+          uint64_t hb = 0;
+          for (const auto& x : tail) hb += x.len;
+          const double hms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
+          (void)hipStreamSynchronize(c->stream);
+          const double gms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
+          fprintf(stderr, "tail: window chunks %lu host %zu (%.1f MB, cut %lu) host %.2f ms, GPU done %.2f ms\n",
+                  (unsigned long)ends.size(), tail.size(), hb / 1e6, (unsigned long)da.skip_above, hms, gms);
+        }
+#endif
       } else {
         rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
         if (rc) return drain(c, pf, rc);
