@@ -550,6 +550,12 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   const int K = dsx_ctx::kIdxSlots;
   Prefetcher pf(fill_shifted, &sh, L, piece, c->idx_slots, K, c->index_readers);
   uint64_t k = 0, i0 = 0;
+  // the host tail of the last window, as in run_index (the list is known here)
+  const bool tail_on = algo == DSX_DIGEST_SHA512_256 &&
+                       (c->index_host_tail > 0 || (c->index_host_tail < 0 && host_sha_vec()));
+  std::vector<TailChunk> tail;
+  std::vector<uint8_t> tail_ids;
+  c->stats.host_tail_chunks = 0;
   for (uint64_t w = 0; w < nwin; ++w) {
     const uint64_t ws = w * W, wl = std::min(W, L - ws);
     uint8_t* buf = c->idx_win[w & 1].p;
@@ -586,8 +592,20 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       da.first_start = i0 == 0 ? 0 : ends[i0 - 1] - start;
       da.n = i1 - i0;
       da.ids = c->dg_ids.p + i0 * 32;
+      const int threads = (int)std::max(1u, std::min<unsigned>(kTailThreads, std::thread::hardware_concurrency()));
+      if (tail_on && w + 1 == nwin) {
+        std::vector<uint64_t> rel(i1 - i0);
+        for (uint64_t i = i0; i < i1; ++i) rel[i - i0] = ends[i] - start;
+        tail = plan_tail(c, rel, i0, da.first_start, threads, &da.skip_above);
+      }
       rc = launch_digest(c, da, i1 - i0, algo);
       if (rc) return drain(c, pf, rc);
+      if (!tail.empty()) {  // the host's share while the GPU hashes the rest
+        tail_ids.assign(32 * tail.size(), 0);
+        rc = hash_tail(fill_shifted, &sh, tail, tail_ids.data(), threads);
+        if (rc) return drain(c, pf, rc);
+        c->stats.host_tail_chunks = tail.size();
+      }
     } else if (k >= 1) {  // (the window's buffer is free once its copies landed)
       hipError_t e = hipStreamWaitEvent(c->stream, c->idx_copy_ev[(k - 1) % K], 0);
       if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: wait"));
@@ -600,6 +618,8 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   HIPCHK(c, hipStreamSynchronize(c->copy_stream));
   HIPCHK(c, hipMemcpyAsync(out_ids, c->dg_ids.p, n * 32, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (size_t j = 0; j < tail.size(); ++j)  // (the GPU skipped these)
+    memcpy(out_ids + 32 * tail[j].idx, tail_ids.data() + 32 * j, 32);
   return DSX_OK;
 }
 

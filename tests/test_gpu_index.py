@@ -109,7 +109,8 @@ def test_index_host_tail(tmp_path, monkeypatch, tail):
     GPU digest skips them): forced for every chunk above 64 KiB, off, and the
     default (the pipeline's own cut).  Several windows, so only the last one
     has a tail; from a file and from host memory.  The cut list equals the
-    oracle's and every ID hashlib's; the stats count the host's chunks."""
+    oracle's and every ID hashlib's, and so are VerifyIndex's IDs of the same
+    list (dsx_ids_fd / dsx_ids_host); the stats count the host's chunks."""
     import desync_amd
     from desync_amd import _lib
     monkeypatch.setenv("DSX_INDEX_HOST_TAIL", tail)
@@ -133,6 +134,19 @@ def test_index_host_tail(tmp_path, monkeypatch, tail):
         ends2, ids2 = desync_amd.index_host(data, MIN, AVG, MAX, ctx=ctx)
         assert np.array_equal(ends2, ref) and [bytes(x) for x in ids2] == want
         assert ctx.stats().host_tail_chunks == n_host
+        # VerifyIndex's IDs of a given list (dsx_ids_fd / dsx_ids_host): the same tail
+        fd = os.open(str(f), os.O_RDONLY)
+        try:
+            ids3 = desync_amd.make.ids_fd(fd, 0, ref, ctx=ctx)
+        finally:
+            os.close(fd)
+        assert [bytes(x) for x in ids3] == want
+        ids4 = desync_amd.make.ids_host(data, 0, ref, ctx=ctx)
+        assert [bytes(x) for x in ids4] == want
+        if tail == "0":
+            assert ctx.stats().host_tail_chunks == 0
+        elif tail == "65536":
+            assert ctx.stats().host_tail_chunks > 0
     finally:
         ctx.close()
     if tail == "0":
