@@ -58,10 +58,12 @@ EXPORTS = (
     "dsx_get_stats", "dsx_debug_trace", "dsx_index_fd", "dsx_index_host", "dsx_copy",
     "dsx_ids_fd", "dsx_ids_host", "dsx_progress", "dsx_shard_resolve_async", "dsx_shard_collect",
     "dsx_ctx_stream", "dsx_stamps_begin", "dsx_stamps_end", "dsx_host_copy",
+    "dsx_host_sha512_256",
 )
 DSX_DIGEST_SHA512_256 = 0
 DSX_DIGEST_SHA256 = 1
 DSX_ENDS_DEVICE = 4
+DSX_HOST_SHA_SCALAR = 1
 
 
 class Params(ctypes.Structure):
@@ -227,6 +229,7 @@ def lib():
             "dsx_stamps_begin": (i32, [vp, u64]),
             "dsx_stamps_end": (i32, [vp, vp, u64, P(u64)]),
             "dsx_host_copy": (i32, [vp, vp, u64, i32]),
+            "dsx_host_sha512_256": (i32, [vp, vp, u64, vp, i32, i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -12,8 +12,10 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "dsx_engine.h"
 
@@ -204,4 +206,40 @@ DSX_AVX512 void host_sha512_256_x8(const uint8_t* const p[8], const uint64_t n[8
     for (int j = 0; j < 4; ++j)
       for (int k = 0; k < 8; ++k) out[i][8 * j + k] = (uint8_t)(hv[j][i] >> (56 - 8 * k));
   }
+}
+
+// The same from C (include/dsx.h): groups of 8 longest first over the host pool.
+extern "C" int dsx_host_sha512_256(const uint8_t* const* ptrs, const uint64_t* lens, uint64_t n,
+                                   uint8_t* ids, int threads, int flags) {
+  if (n && (!ptrs || !lens || !ids)) return DSX_E_INVAL;
+  if (flags & ~DSX_HOST_SHA_SCALAR) return DSX_E_INVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (!ptrs[i] && lens[i]) return DSX_E_INVAL;
+  if (!n) return DSX_OK;
+  const bool vec = !(flags & DSX_HOST_SHA_SCALAR) && host_sha_vec();
+  std::vector<uint64_t> order(n);
+  for (uint64_t i = 0; i < n; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return lens[x] > lens[y]; });
+  const uint64_t per = vec ? 8 : 1, groups = (n + per - 1) / per;
+  std::atomic<uint64_t> next{0};
+  host_parallel((int)std::min<uint64_t>((uint64_t)std::max(1, threads), groups), [&](int) {
+    for (uint64_t g; (g = next.fetch_add(1)) < groups;) {
+      if (!vec) {
+        const uint64_t i = order[g];
+        host_sha512_256_one(ptrs[i], lens[i], ids + 32 * i);
+        continue;
+      }
+      const uint8_t* p[8];
+      uint64_t l[8];
+      uint8_t* o[8];
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t j = 8 * g + k;
+        p[k] = j < n ? ptrs[order[j]] : nullptr;
+        l[k] = j < n ? lens[order[j]] : UINT64_MAX;
+        o[k] = j < n ? ids + 32 * order[j] : nullptr;
+      }
+      host_sha512_256_x8(p, l, o);
+    }
+  });
+  return DSX_OK;
 }

@@ -211,6 +211,15 @@ const uint8_t *dsx_stream_chunk_id(dsx_ctx_t *ctx);
  * (<= 1: the calling thread alone).  dst and src must not overlap.  No
  * context; no GPU. */
 int dsx_host_copy(void *dst, const void *src, uint64_t n, int threads);
+/* Digest.Sum (digest.go:22, SHA-512/256) of n host messages ptrs[i] of lens[i]
+ * bytes into ids[32 i], on up to `threads` host threads: 8 messages per set of
+ * AVX-512 registers, longest first (the scalar form without AVX-512, or with
+ * DSX_HOST_SHA_SCALAR in flags).  The same code hashes the long chunks of an
+ * index call's last window on the host (DSX_INDEX_HOST_TAIL).
+ * No context; no GPU. */
+#define DSX_HOST_SHA_SCALAR 1
+int dsx_host_sha512_256(const uint8_t *const *ptrs, const uint64_t *lens, uint64_t n, uint8_t *ids,
+                        int threads, int flags);
 
 /* ---- multi-GPU shards (split-and-align across ranks) ------------------------
  * A blob of total length `total` is range-sharded; rank r holds

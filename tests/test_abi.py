@@ -15,7 +15,7 @@ HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 def declared_functions():
     txt = open(HDR).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(dsx_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(dsx_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_and_binding_agree():

@@ -246,6 +246,36 @@ def test_host_copy_pool():
     assert bytes(v) == src[:(5 << 20) + 7].tobytes()
 
 
+def test_host_sha512_256():
+    """dsx_host_sha512_256, the host SHA-512/256 of the index pipeline's tail
+    (digest.go:22): the AVX-512 multi-buffer form (when the CPU has it) and
+    the scalar form against hashlib, over the padding edge lengths (111, 112,
+    127, 128, 239, 240 ...), empty messages, groups of 8 with ragged lengths
+    and a thread count above the group count.  Host only, no GPU."""
+    import ctypes
+    import hashlib
+
+    import numpy as np
+
+    from desync_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(12)
+    lens = [0, 1, 55, 111, 112, 113, 127, 128, 129, 239, 240, 241, 256, 1000, 65536, 262144]
+    lens += [int(x) for x in rng.integers(0, 300000, 45)]
+    bufs = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+    ptrs = (ctypes.c_void_p * len(bufs))(*[b.ctypes.data if b.size else None for b in bufs])
+    ln = (ctypes.c_uint64 * len(bufs))(*lens)
+    want = [hashlib.new("sha512_256", b.tobytes()).digest() for b in bufs]
+    for flags in (0, _lib.DSX_HOST_SHA_SCALAR):
+        for threads in (1, 3, 64):
+            out = np.zeros(32 * len(bufs), np.uint8)
+            assert L.dsx_host_sha512_256(ptrs, ln, len(bufs), out.ctypes.data, threads, flags) == 0
+            got = [out[32 * i:32 * i + 32].tobytes() for i in range(len(bufs))]
+            assert got == want, (flags, threads)
+    assert L.dsx_host_sha512_256(ptrs, ln, len(bufs), None, 1, 0) == _lib.DSX_E_INVAL
+    assert L.dsx_host_sha512_256(ptrs, ln, len(bufs), out.ctypes.data, 1, 4) == _lib.DSX_E_INVAL
+
+
 def test_chunkstream_store_workers():
     """ChunkStream's store workers over blocks of chunks (a stand-in chunker,
     no GPU): an ID repeated within and across hand-offs is stored once (the
