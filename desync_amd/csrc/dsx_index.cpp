@@ -26,6 +26,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <memory>
 #include <cerrno>
 #include <condition_variable>
 #include <cstring>
@@ -294,6 +295,127 @@ int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* i
   return err.load();
 }
 
+// The long chunks of a one-window call hashed on the host while the file is
+// still being read: a thread follows the chain state each stitch publishes
+// (HostState.total, seq written last), copies the newly final cut ends to the
+// host and hashes the chunks longer than `cut` (read again through the
+// call's fill function) on the host pool.  After the read, the GPU digest
+// skips those chunks (DigestArgs.skip_above = cut) and hashes the rest, a
+// chain of at most `cut` bytes; finish() hands the feeder the final count.
+class TailFeeder {
+ public:
+  TailFeeder(dsx_ctx* c, FillFn fill, void* ud, uint64_t len, uint64_t cut, int threads,
+             uint64_t seq0)
+      : c_(c), fill_(fill), ud_(ud), len_(len), cut_(cut), threads_(threads), seq0_(seq0) {
+    th_ = std::thread([this] { run(); });
+  }
+  ~TailFeeder() { stop(); }
+  void finish(uint64_t total) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      final_ = total;
+      have_final_ = true;
+    }
+    cv_.notify_all();
+  }
+  // joins; the hashed chunks and their IDs, or an error
+  int join() {
+    if (th_.joinable()) th_.join();
+    return err_;
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  std::vector<TailChunk> chunks;
+  std::vector<uint8_t> ids;
+
+ private:
+  // cuts the device has published as final, 0 if none of this call yet
+  uint64_t published() const {
+    const volatile HostState* h = (const volatile HostState*)c_->h_state;
+    const uint64_t q0 = h->seq;
+    const uint64_t t = h->total;
+    const uint64_t q1 = h->seq;
+    return (q0 == q1 && q0 > seq0_) ? t : 0;
+  }
+  void run() {
+    if (hipSetDevice(c_->device) != hipSuccess) {
+      err_ = DSX_E_HIP;
+      return;
+    }
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      err_ = DSX_E_HIP;
+      return;
+    }
+    std::vector<uint64_t> e;
+    uint64_t seen = 0, prev = 0;
+    while (true) {
+      uint64_t target;
+      bool last;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait_for(g, std::chrono::microseconds(200), [&] { return stop_ || have_final_; });
+        if (stop_) break;
+        last = have_final_;
+        target = last ? final_ : std::max(seen, published());
+      }
+      if (target > seen) {
+        e.resize(target - seen);
+        if (hipMemcpyAsync(e.data(), c_->out.p + seen, e.size() * 8, hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+          err_ = DSX_E_HIP;
+          break;
+        }
+        std::vector<TailChunk> batch;
+        for (uint64_t i = 0; i < e.size(); ++i) {
+          const uint64_t st = i ? e[i - 1] : prev;
+          // (a call that overflows its candidate slots reruns and drops these:
+          // never read outside the source for them)
+          if (e[i] > st && e[i] <= len_ && e[i] - st > cut_) batch.push_back({seen + i, st, e[i] - st});
+        }
+        prev = e.back();
+        seen = target;
+        if (!batch.empty()) {
+          std::sort(batch.begin(), batch.end(),
+                    [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
+          const size_t at = chunks.size();
+          ids.resize(32 * (at + batch.size()));
+          const int rc = hash_tail(fill_, ud_, batch, ids.data() + 32 * at, threads_);
+          if (rc) {
+            err_ = rc;
+            break;
+          }
+          chunks.insert(chunks.end(), batch.begin(), batch.end());
+        }
+      }
+      if (last) break;
+    }
+    (void)hipStreamDestroy(s);
+  }
+  dsx_ctx* c_;
+  FillFn fill_;
+  void* ud_;
+  uint64_t len_;
+  uint64_t cut_;
+  int threads_;
+  uint64_t seq0_;
+  std::thread th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool stop_ = false, have_final_ = false;
+  uint64_t final_ = 0;
+  int err_ = DSX_OK;
+};
+constexpr uint64_t kFeedCut = 64ull << 10;  // the GPU keeps chunks up to this (~3.8 ms chain)
+constexpr int kFeedThreads = 11;            // (+ the 4 readers and the calling thread)
+
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
               uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {
   HIPCHK(c, hipSetDevice(c->device));
@@ -368,6 +490,16 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
                          (c->index_host_tail > 0 || (c->index_host_tail < 0 && host_sha_vec()));
     std::vector<TailChunk> tail;
     std::vector<uint8_t> tail_ids;
+    // one window: its long chunks are hashed on the host during the read
+    std::unique_ptr<TailFeeder> feed;
+    const uint64_t feed_cut = c->index_host_tail > 0 ? (uint64_t)c->index_host_tail : kFeedCut;
+    if (tail_on && nwin == 1) {
+      int fth = kFeedThreads;
+#if DSX_DIAG
+      if (const char* v = getenv("DSX_FEED_THREADS")) fth = std::max(1, std::min(64, atoi(v)));
+#endif
+      feed.reset(new TailFeeder(c, fill, ud, len, feed_cut, fth, c->piece_seq));
+    }
     for (w = 0; w < nwin; ++w) {
       ws = w * W;
       wl = std::min(W, len - ws);
@@ -435,6 +567,34 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           e = hipMemcpy(ends.data(), c->out.p + i0, (i1 - i0) * 8, hipMemcpyDeviceToHost);
         if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: tail ends"));
         const int threads = (int)std::max(1u, std::min<unsigned>(kTailThreads, std::thread::hardware_concurrency()));
+        if (feed) {  // the feeder has the long chunks: the GPU the rest
+          da.skip_above = feed_cut;
+          rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
+          if (rc) return drain(c, pf, rc);
+#if DSX_DIAG
+          const auto tf0 = std::chrono::steady_clock::now();
+#endif
+          feed->finish(i1);
+          rc = feed->join();
+          if (rc) return drain(c, pf, rc);
+          tail = std::move(feed->chunks);
+          tail_ids = std::move(feed->ids);
+          c->stats.host_tail_chunks = tail.size();
+#if DSX_DIAG
+          if (getenv("DSX_TAIL_LOG")) {
+            const double hms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
+            (void)hipStreamSynchronize(c->stream);
+            const double gms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
+            fprintf(stderr, "feed: chunks %lu host %zu (cut %lu) host done %.2f ms, GPU done %.2f ms\n",
+                    (unsigned long)i1, tail.size(), (unsigned long)feed_cut, hms, gms);
+          }
+#endif
+          e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
+          if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
+          continue;
+        }
         tail = plan_tail(c, ends, i0, snap[1], threads, &da.skip_above);
         rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
         if (rc) return drain(c, pf, rc);

@@ -102,19 +102,23 @@ def test_index_fd_reader_threads(tmp_path, monkeypatch, readers):
     assert [bytes(x) for x in ids] == _ids(data, ref, "sha512-256")
 
 
-@pytest.mark.parametrize("tail", ["65536", "0", "-1"])
-def test_index_host_tail(tmp_path, monkeypatch, tail):
+@pytest.mark.parametrize("tail,window", [("65536", 16 << 20), ("0", 16 << 20), ("-1", 16 << 20),
+                                         ("100000", None), ("-1", None)])
+def test_index_host_tail(tmp_path, monkeypatch, tail, window):
     """DSX_INDEX_HOST_TAIL (make.go:223's Digest.Sum for the last window's
     longest chunks on the host, AVX-512 multi-buffer SHA-512/256, while the
     GPU digest skips them): forced for every chunk above 64 KiB, off, and the
-    default (the pipeline's own cut).  Several windows, so only the last one
-    has a tail; from a file and from host memory.  The cut list equals the
+    default (the pipeline's own cut), over several windows (only the last one
+    has a tail); and in one window, where a feeder thread hashes the long
+    chunks while the file is still being read (forced above 100000 bytes, and
+    the default 64 KiB).  From a file and from host memory.  The cut list equals the
     oracle's and every ID hashlib's, and so are VerifyIndex's IDs of the same
     list (dsx_ids_fd / dsx_ids_host); the stats count the host's chunks."""
     import desync_amd
     from desync_amd import _lib
     monkeypatch.setenv("DSX_INDEX_HOST_TAIL", tail)
-    monkeypatch.setenv("DSX_INDEX_WINDOW", str(16 << 20))
+    if window:
+        monkeypatch.setenv("DSX_INDEX_WINDOW", str(window))
     data = o.synth_uniform(47, 0, (40 << 20) + 777)
     f = tmp_path / "blob"
     f.write_bytes(data.tobytes())
@@ -145,12 +149,18 @@ def test_index_host_tail(tmp_path, monkeypatch, tail):
         assert [bytes(x) for x in ids4] == want
         if tail == "0":
             assert ctx.stats().host_tail_chunks == 0
-        elif tail == "65536":
+        elif tail != "-1":
             assert ctx.stats().host_tail_chunks > 0
     finally:
         ctx.close()
     if tail == "0":
         assert n_host == 0
+    elif window is None:  # one window: the feeder takes every chunk above the cut
+        cut = int(tail) if tail != "-1" else 65536
+        lens = np.diff(np.concatenate([[0], ref.astype(np.int64)]))
+        avx512 = "avx512f" in open("/proc/cpuinfo").read() and "avx512bw" in open("/proc/cpuinfo").read()
+        if tail != "-1" or avx512:  # (auto needs AVX-512)
+            assert n_host == int(np.sum(lens > cut)) > 0
     elif tail == "65536":
         assert 0 < n_host < long_chunks  # (the last window's share of them)
     else:
