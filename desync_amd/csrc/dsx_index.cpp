@@ -716,6 +716,29 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   std::vector<TailChunk> tail;
   std::vector<uint8_t> tail_ids;
   c->stats.host_tail_chunks = 0;
+  // One window: the list is known up front, so the host hashes its long
+  // chunks from the start, beside the read (the tail feeder of run_index
+  // without the wait for the stitch); the digest skips them.
+  const uint64_t early_cut = c->index_host_tail > 0 ? (uint64_t)c->index_host_tail : kFeedCut;
+  std::vector<TailChunk> early;
+  std::vector<uint8_t> early_ids;
+  int early_rc = DSX_OK;
+  struct Joiner {
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } early_th;
+  if (tail_on && nwin == 1) {
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t s0 = i ? ends[i - 1] - start : 0, e0 = ends[i] - start;
+      if (e0 - s0 > early_cut) early.push_back({i, s0, e0 - s0});
+    }
+    std::sort(early.begin(), early.end(), [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
+    early_ids.assign(32 * early.size(), 0);
+    if (!early.empty())
+      early_th.t = std::thread([&] { early_rc = hash_tail(fill_shifted, &sh, early, early_ids.data(), kFeedThreads); });
+  }
   for (uint64_t w = 0; w < nwin; ++w) {
     const uint64_t ws = w * W, wl = std::min(W, L - ws);
     uint8_t* buf = c->idx_win[w & 1].p;
@@ -753,6 +776,20 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       da.n = i1 - i0;
       da.ids = c->dg_ids.p + i0 * 32;
       const int threads = (int)std::max(1u, std::min<unsigned>(kTailThreads, std::thread::hardware_concurrency()));
+      if (tail_on && w + 1 == nwin && nwin == 1) {
+        da.skip_above = early_cut;
+        rc = launch_digest(c, da, i1 - i0, algo);
+        if (rc) return drain(c, pf, rc);
+        if (early_th.t.joinable()) early_th.t.join();
+        if (early_rc) return drain(c, pf, early_rc);
+        tail = std::move(early);
+        tail_ids = std::move(early_ids);
+        c->stats.host_tail_chunks = tail.size();
+        hipError_t e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
+        if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: record"));
+        i0 = i1;
+        continue;
+      }
       if (tail_on && w + 1 == nwin) {
         std::vector<uint64_t> rel(i1 - i0);
         for (uint64_t i = i0; i < i1; ++i) rel[i - i0] = ends[i] - start;
