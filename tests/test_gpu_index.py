@@ -349,16 +349,20 @@ def test_index_progress_granularity(tmp_path):
     assert all(v in ends for v in sets)
 
 
-def test_index_partial_on_io_error(tmp_path, monkeypatch):
+@pytest.mark.parametrize("window", [1 << 20, None])
+def test_index_partial_on_io_error(tmp_path, monkeypatch, window):
     """A read error mid-file (the range runs past the end of the file): the
     error carries the confirmed prefix -- IndexFromFile returns the chunks
     assembled so far with chunkErr (make.go:133-162) -- cut for cut the
-    oracle's chain and ID for ID hashlib."""
+    oracle's chain and ID for ID hashlib.  Over many windows, and in one (the
+    tail feeder hashing beside the read when the error comes)."""
     import desync_amd
     from desync_amd import _lib
-    monkeypatch.setenv("DSX_INDEX_WINDOW", str(1 << 20))
+    if window:
+        monkeypatch.setenv("DSX_INDEX_WINDOW", str(window))
     monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 18))
-    data = o.synth_uniform(44, 0, (24 << 20) + 5)
+    # (one window confirms cuts every 32 MiB scan step: a file of several)
+    data = o.synth_uniform(44, 0, ((24 if window else 72) << 20) + 5)
     f = tmp_path / "blob"
     f.write_bytes(data.tobytes())
     ref = o.chunk_stream(data, MIN, AVG, MAX)
@@ -373,7 +377,7 @@ def test_index_partial_on_io_error(tmp_path, monkeypatch):
             assert e.code == _lib.DSX_E_IO
             n = len(e.ends)
             assert 0 < n < ref.size and np.array_equal(e.ends, ref[:n])
-            assert int(e.ends[-1]) > data.size - 4 * MAX - (2 << 20)
+            assert int(e.ends[-1]) > data.size - 4 * MAX - ((2 if window else 32) << 20)
             assert [bytes(x) for x in e.ids] == _ids(data, ref[:n], algo)
             # the next call on the context is unaffected
             ends, _ = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
@@ -383,13 +387,16 @@ def test_index_partial_on_io_error(tmp_path, monkeypatch):
         ctx.close()
 
 
-def test_index_partial_on_cancel(tmp_path, monkeypatch):
+@pytest.mark.parametrize("window", [8 << 20, None])
+def test_index_partial_on_cancel(tmp_path, monkeypatch, window):
     """Interrupted mid-file (make.go:201-203): cancelled from the progress
     callback at the first confirmed chunk, IndexFromFile raises Interrupted
-    carrying a non-empty strict prefix of the chain with its IDs."""
+    carrying a non-empty strict prefix of the chain with its IDs (many
+    windows, and one: the tail feeder running)."""
     import desync_amd
     from desync_amd import _lib
-    monkeypatch.setenv("DSX_INDEX_WINDOW", str(8 << 20))
+    if window:
+        monkeypatch.setenv("DSX_INDEX_WINDOW", str(window))
     monkeypatch.setenv("DSX_INDEX_SLOT", str(1 << 20))
     data = o.synth_uniform(45, 0, 768 << 20)
     f = tmp_path / "blob"
