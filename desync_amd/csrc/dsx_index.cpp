@@ -413,8 +413,13 @@ class TailFeeder {
   uint64_t final_ = 0;
   int err_ = DSX_OK;
 };
-constexpr uint64_t kFeedCut = 64ull << 10;  // the GPU keeps chunks up to this (~3.8 ms chain)
-constexpr int kFeedThreads = 11;            // (+ the 4 readers and the calling thread)
+// the GPU keeps chunks up to kFeedCut (a ~1.9 ms chain at the end); the host
+// the rest, ~85 % of the bytes, on kFeedThreads beside the 4 readers: more
+// threads than the box's 16-CPU share, but the host's rate is what bounds the
+// end (tools/feed_ab.py, profiles/r05bi-r05bk: 11 threads at 64 KiB 0.78-0.82 x
+// dsx_cut_fd, 24 at 32 KiB 0.85-0.88, fewer threads or 48 KiB no better)
+constexpr uint64_t kFeedCut = 32ull << 10;
+constexpr int kFeedThreads = 24;
 
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
               uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {
@@ -446,6 +451,9 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   const int K = dsx_ctx::kIdxSlots;
 
   ProgressScope prog(c, len);
+#if DSX_DIAG
+  const auto call_t0 = std::chrono::steady_clock::now();
+#endif
   for (int attempt = 0; attempt < 2; ++attempt) {
     CallCfg cc{p, len, 0, kRound, c->out.p, need, attempt == 1};
     rc = reset_state(c, 0);
@@ -535,6 +543,11 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           c->timing = true;
           if (rc) return drain(c, pf, rc);
           scanned = end;
+#if DSX_DIAG
+          if (end == len && getenv("DSX_TAIL_LOG"))
+            fprintf(stderr, "index: last piece enqueued %.2f ms into the call\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
+#endif
         }
       }
       // the window's finished chunks: [snap[w].total, snap[w+1].total) from
@@ -573,6 +586,9 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           if (rc) return drain(c, pf, rc);
 #if DSX_DIAG
           const auto tf0 = std::chrono::steady_clock::now();
+          if (getenv("DSX_TAIL_LOG"))
+            fprintf(stderr, "feed: last piece stitched %.2f ms into the call, %zu host chunks by then\n",
+                    std::chrono::duration<double, std::milli>(tf0 - call_t0).count(), feed->chunks.size());
 #endif
           feed->finish(i1);
           rc = feed->join();
@@ -637,6 +653,11 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       c->err = "index: stitch error";
       return DSX_E_INTERNAL;
     }
+#if DSX_DIAG
+    if (getenv("DSX_TAIL_LOG"))
+      fprintf(stderr, "index: done %.2f ms into the call\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
+#endif
     c->stats.chunks = st.total;
     c->stats.repaired_segments = st.repaired;
     c->stats.chunks_discarded = st.discarded;

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""In-process A/B of IndexFromFile's one-window tail feeder (dsx_index.cpp,
+TailFeeder): a 1 GiB page-cache file, `dsx_index_fd` under several feeder
+settings and `dsx_cut_fd` (the same read without IDs), the cases alternating
+call by call so that the box's drift in page-cache read speed falls on all of
+them alike.  Needs the diagnostic build for DSX_FEED_THREADS:
+
+  DSX_LIB_PATH=desync_amd/libdsx_diag.so python3 tools/feed_ab.py [rounds] [case ...]
+
+A case is name=THREADS:CUT (CUT -1 = the default 64 KiB, else DSX_INDEX_HOST_TAIL)
+or `cut` (dsx_cut_fd).  Prints one JSON line: per case the median, min and max
+GiB/s and the median ratio to dsx_cut_fd of the same round.
+"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import desync_amd  # noqa: E402
+from desync_amd import _lib  # noqa: E402
+
+MIN, AVG, MAX = 16 << 10, 64 << 10, 256 << 10
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    cases = sys.argv[2:] or ["t11=11:-1", "t8=8:-1", "t11c96=11:98304", "off=11:0", "cut"]
+    n = 1 << 30
+    rng = np.random.default_rng(7)
+    fd, path = tempfile.mkstemp(prefix="dsx_feed_")
+    res = {c.split("=")[0]: [] for c in cases}
+    ratio = {c.split("=")[0]: [] for c in cases}
+    try:
+        with os.fdopen(fd, "wb") as f:
+            for _ in range(4):
+                f.write(rng.integers(0, 256, 256 << 20, dtype=np.uint8).tobytes())
+        # one context per cut (DSX_INDEX_HOST_TAIL is read when a context is
+        # made; DSX_FEED_THREADS at each call): switching settings through the
+        # pool would close and remake them
+        ctxs = {}
+        for c in cases:
+            cut = c.split("=")[1].split(":")[1] if c != "cut" else "-1"
+            if cut not in ctxs:
+                os.environ["DSX_INDEX_HOST_TAIL"] = cut
+                ctxs[cut] = _lib.Context(0)
+        fdr = os.open(path, os.O_RDONLY)
+        try:
+            for r in range(rounds + 1):  # (round 0 warms the contexts, not counted)
+                times = {}
+                for c in cases:
+                    name = c.split("=")[0]
+                    if c == "cut":
+                        t0 = time.perf_counter()
+                        desync_amd.cut_fd(fdr, MIN, AVG, MAX, ctx=ctxs["-1"])
+                    else:
+                        th, cut = c.split("=")[1].split(":")
+                        os.environ["DSX_FEED_THREADS"] = th
+                        t0 = time.perf_counter()
+                        desync_amd.index_fd(fdr, MIN, AVG, MAX, ctx=ctxs[cut])
+                    times[name] = time.perf_counter() - t0
+                if r == 0:
+                    continue
+                for name, t in times.items():
+                    res[name].append(n / t / (1 << 30))
+                    if "cut" in times:
+                        ratio[name].append(times["cut"] / t)
+        finally:
+            os.close(fdr)
+            for ctx in ctxs.values():
+                ctx.close()
+    finally:
+        os.unlink(path)
+    out = {}
+    for name, v in res.items():
+        out[name] = {"gibs_median": round(float(np.median(v)), 2), "gibs_min": round(min(v), 2),
+                     "gibs_max": round(max(v), 2),
+                     "ratio_to_cut_fd_median": round(float(np.median(ratio[name])), 3) if ratio[name] else None}
+    print(json.dumps({"tool": "feed_ab", "gib": 1, "rounds": rounds, "cases": cases, "results": out}))
+
+
+if __name__ == "__main__":
+    main()
