@@ -587,8 +587,8 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #if DSX_DIAG
           const auto tf0 = std::chrono::steady_clock::now();
           if (getenv("DSX_TAIL_LOG"))
-            fprintf(stderr, "feed: last piece stitched %.2f ms into the call, %zu host chunks by then\n",
-                    std::chrono::duration<double, std::milli>(tf0 - call_t0).count(), feed->chunks.size());
+            fprintf(stderr, "feed: last piece stitched %.2f ms into the call\n",
+                    std::chrono::duration<double, std::milli>(tf0 - call_t0).count());
 #endif
           feed->finish(i1);
           rc = feed->join();
