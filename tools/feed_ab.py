@@ -7,8 +7,9 @@ them alike.  Needs the diagnostic build for DSX_FEED_THREADS:
 
   DSX_LIB_PATH=desync_amd/libdsx_diag.so python3 tools/feed_ab.py [rounds] [case ...]
 
-A case is name=THREADS:CUT (CUT -1 = the default 64 KiB, else DSX_INDEX_HOST_TAIL)
-or `cut` (dsx_cut_fd).  Prints one JSON line: per case the median, min and max
+A case is name=THREADS:CUT[:READERS] (CUT -1 = the default, else
+DSX_INDEX_HOST_TAIL; READERS = DSX_INDEX_READERS, default 4) or `cut[:READERS]`
+(dsx_cut_fd).  Prints one JSON line: per case the median, min and max
 GiB/s and the median ratio to dsx_cut_fd of the same round.
 """
 import json
@@ -43,32 +44,38 @@ def main():
         # one context per cut (DSX_INDEX_HOST_TAIL is read when a context is
         # made; DSX_FEED_THREADS at each call): switching settings through the
         # pool would close and remake them
+        def key(c):
+            if c.startswith("cut"):
+                f = c.split(":")
+                return ("-1", f[1] if len(f) > 1 else "4")
+            f = c.split("=")[1].split(":")
+            return (f[1], f[2] if len(f) > 2 else "4")
+
         ctxs = {}
         for c in cases:
-            cut = c.split("=")[1].split(":")[1] if c != "cut" else "-1"
-            if cut not in ctxs:
-                os.environ["DSX_INDEX_HOST_TAIL"] = cut
-                ctxs[cut] = _lib.Context(0)
+            k = key(c)
+            if k not in ctxs:
+                os.environ["DSX_INDEX_HOST_TAIL"], os.environ["DSX_INDEX_READERS"] = k
+                ctxs[k] = _lib.Context(0)
         fdr = os.open(path, os.O_RDONLY)
         try:
             for r in range(rounds + 1):  # (round 0 warms the contexts, not counted)
                 times = {}
                 for c in cases:
                     name = c.split("=")[0]
-                    if c == "cut":
+                    if c.startswith("cut"):
                         t0 = time.perf_counter()
-                        desync_amd.cut_fd(fdr, MIN, AVG, MAX, ctx=ctxs["-1"])
+                        desync_amd.cut_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
                     else:
-                        th, cut = c.split("=")[1].split(":")
-                        os.environ["DSX_FEED_THREADS"] = th
+                        os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
                         t0 = time.perf_counter()
-                        desync_amd.index_fd(fdr, MIN, AVG, MAX, ctx=ctxs[cut])
+                        desync_amd.index_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
                     times[name] = time.perf_counter() - t0
                 if r == 0:
                     continue
                 for name, t in times.items():
                     res[name].append(n / t / (1 << 30))
-                    if "cut" in times:
+                    if "cut" in times:  # (the case named `cut`: dsx_cut_fd, default readers)
                         ratio[name].append(times["cut"] / t)
         finally:
             os.close(fdr)
