@@ -413,13 +413,14 @@ class TailFeeder {
   uint64_t final_ = 0;
   int err_ = DSX_OK;
 };
-// the GPU keeps chunks up to kFeedCut (a ~1.9 ms chain at the end); the host
-// the rest, ~85 % of the bytes, on kFeedThreads beside the 4 readers: more
+// the GPU keeps chunks up to kFeedCut (a ~1.7 ms chain at the end); the host
+// the rest, ~87 % of the bytes, on kFeedThreads beside the 4 readers: more
 // threads than the box's 16-CPU share, but the host's rate is what bounds the
-// end (tools/feed_ab.py, profiles/r05bi-r05bk: 11 threads at 64 KiB 0.78-0.82 x
-// dsx_cut_fd, 24 at 32 KiB 0.85-0.88, fewer threads or 48 KiB no better)
-constexpr uint64_t kFeedCut = 32ull << 10;
-constexpr int kFeedThreads = 24;
+// end (tools/feed_ab.py, profiles/r05bi-r05bp: 11 threads at 64 KiB 0.75-0.82 x
+// dsx_cut_fd, 24 at 32 KiB 0.78-0.89, 28 at 28 KiB 0.87-0.88; fewer threads,
+// 32 of them, or 40-48 KiB no better)
+constexpr uint64_t kFeedCut = 28ull << 10;
+constexpr int kFeedThreads = 28;
 
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
               uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {

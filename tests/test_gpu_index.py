@@ -111,7 +111,7 @@ def test_index_host_tail(tmp_path, monkeypatch, tail, window):
     default (the pipeline's own cut), over several windows (only the last one
     has a tail); and in one window, where a feeder thread hashes the long
     chunks while the file is still being read (forced above 100000 bytes, and
-    the default 32 KiB).  From a file and from host memory.  The cut list equals the
+    the default 28 KiB).  From a file and from host memory.  The cut list equals the
     oracle's and every ID hashlib's, and so are VerifyIndex's IDs of the same
     list (dsx_ids_fd / dsx_ids_host); the stats count the host's chunks."""
     import desync_amd
@@ -156,7 +156,7 @@ def test_index_host_tail(tmp_path, monkeypatch, tail, window):
     if tail == "0":
         assert n_host == 0
     elif window is None:  # one window: the feeder takes every chunk above the cut
-        cut = int(tail) if tail != "-1" else 32768
+        cut = int(tail) if tail != "-1" else 28672
         lens = np.diff(np.concatenate([[0], ref.astype(np.int64)]))
         avx512 = "avx512f" in open("/proc/cpuinfo").read() and "avx512bw" in open("/proc/cpuinfo").read()
         if tail != "-1" or avx512:  # (auto needs AVX-512)

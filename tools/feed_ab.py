@@ -61,7 +61,9 @@ def main():
         try:
             for r in range(rounds + 1):  # (round 0 warms the contexts, not counted)
                 times = {}
-                for c in cases:
+                # (the order rotates from round to round: no case always
+                # follows the same one)
+                for c in cases[r % len(cases):] + cases[:r % len(cases)]:
                     name = c.split("=")[0]
                     if c.startswith("cut"):
                         t0 = time.perf_counter()
