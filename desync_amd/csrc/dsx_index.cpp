@@ -758,8 +758,12 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
     }
     std::sort(early.begin(), early.end(), [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
     early_ids.assign(32 * early.size(), 0);
+    int eth = kFeedThreads;
+#if DSX_DIAG
+    if (const char* v = getenv("DSX_FEED_THREADS")) eth = std::max(1, std::min(64, atoi(v)));
+#endif
     if (!early.empty())
-      early_th.t = std::thread([&] { early_rc = hash_tail(fill_shifted, &sh, early, early_ids.data(), kFeedThreads); });
+      early_th.t = std::thread([&, eth] { early_rc = hash_tail(fill_shifted, &sh, early, early_ids.data(), eth); });
   }
   for (uint64_t w = 0; w < nwin; ++w) {
     const uint64_t ws = w * W, wl = std::min(W, L - ws);

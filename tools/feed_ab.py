@@ -9,7 +9,8 @@ them alike.  Needs the diagnostic build for DSX_FEED_THREADS:
 
 A case is name=THREADS:CUT[:READERS] (CUT -1 = the default, else
 DSX_INDEX_HOST_TAIL; READERS = DSX_INDEX_READERS, default 4) or `cut[:READERS]`
-(dsx_cut_fd).  Prints one JSON line: per case the median, min and max
+(dsx_cut_fd); a name starting with `v` times dsx_ids_fd (VerifyIndex) of the
+file's chunk list instead of dsx_index_fd.  Prints one JSON line: per case the median, min and max
 GiB/s and the median ratio to dsx_cut_fd of the same round.
 """
 import json
@@ -59,6 +60,7 @@ def main():
                 ctxs[k] = _lib.Context(0)
         fdr = os.open(path, os.O_RDONLY)
         try:
+            ends, _ = desync_amd.index_fd(fdr, MIN, AVG, MAX)
             for r in range(rounds + 1):  # (round 0 warms the contexts, not counted)
                 times = {}
                 # (the order rotates from round to round: no case always
@@ -68,6 +70,10 @@ def main():
                     if c.startswith("cut"):
                         t0 = time.perf_counter()
                         desync_amd.cut_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
+                    elif c.startswith("v"):  # VerifyIndex's IDs of the list (dsx_ids_fd)
+                        os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
+                        t0 = time.perf_counter()
+                        desync_amd.ids_fd(fdr, 0, ends, ctx=ctxs[key(c)])
                     else:
                         os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
                         t0 = time.perf_counter()
