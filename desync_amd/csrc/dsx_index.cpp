@@ -295,8 +295,8 @@ int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* i
   return err.load();
 }
 
-// The long chunks of a one-window call hashed on the host while the file is
-// still being read: a thread follows the chain state each stitch publishes
+// The long chunks of a call's last window (the whole file up to the window
+// size) hashed on the host while that window is still being read: a thread follows the chain state each stitch publishes
 // (HostState.total, seq written last), copies the newly final cut ends to the
 // host and hashes the chunks longer than `cut` (read again through the
 // call's fill function) on the host pool.  After the read, the GPU digest
@@ -304,9 +304,12 @@ int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* i
 // chain of at most `cut` bytes; finish() hands the feeder the final count.
 class TailFeeder {
  public:
+  // (the last of several windows: start_ev marks the previous window's
+  // snapshot dsnap = {cuts before this window, their last end})
   TailFeeder(dsx_ctx* c, FillFn fill, void* ud, uint64_t len, uint64_t cut, int threads,
-             uint64_t seq0)
-      : c_(c), fill_(fill), ud_(ud), len_(len), cut_(cut), threads_(threads), seq0_(seq0) {
+             uint64_t seq0, hipEvent_t start_ev = nullptr, const uint64_t* dsnap = nullptr)
+      : c_(c), fill_(fill), ud_(ud), len_(len), cut_(cut), threads_(threads), seq0_(seq0),
+        start_ev_(start_ev), dsnap_(dsnap) {
     th_ = std::thread([this] { run(); });
   }
   ~TailFeeder() { stop(); }
@@ -355,6 +358,18 @@ class TailFeeder {
     }
     std::vector<uint64_t> e;
     uint64_t seen = 0, prev = 0;
+    if (start_ev_) {
+      uint64_t sn[2] = {0, 0};
+      if (hipEventSynchronize(start_ev_) != hipSuccess ||
+          hipMemcpyAsync(sn, dsnap_, sizeof sn, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        err_ = DSX_E_HIP;
+        (void)hipStreamDestroy(s);
+        return;
+      }
+      seen = sn[0];
+      prev = sn[1];
+    }
     while (true) {
       uint64_t target;
       bool last;
@@ -406,6 +421,8 @@ class TailFeeder {
   uint64_t cut_;
   int threads_;
   uint64_t seq0_;
+  hipEvent_t start_ev_;
+  const uint64_t* dsnap_;
   std::thread th_;
   std::mutex m_;
   std::condition_variable cv_;
@@ -499,20 +516,34 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
                          (c->index_host_tail > 0 || (c->index_host_tail < 0 && host_sha_vec()));
     std::vector<TailChunk> tail;
     std::vector<uint8_t> tail_ids;
-    // one window: its long chunks are hashed on the host during the read
+    // the last window's long chunks are hashed on the host during its read;
+    // with several windows the feeder starts from the previous window's
+    // snapshot (feed_ev: recorded after it)
+    struct Ev {
+      hipEvent_t e = nullptr;
+      ~Ev() {
+        if (e) (void)hipEventDestroy(e);
+      }
+    } feed_ev;
+    if (tail_on && nwin > 1) HIPCHK(c, hipEventCreateWithFlags(&feed_ev.e, hipEventDisableTiming));
     std::unique_ptr<TailFeeder> feed;
     const uint64_t feed_cut = c->index_host_tail > 0 ? (uint64_t)c->index_host_tail : kFeedCut;
-    if (tail_on && nwin == 1) {
-      int fth = kFeedThreads;
-#if DSX_DIAG
-      if (const char* v = getenv("DSX_FEED_THREADS")) fth = std::max(1, std::min(64, atoi(v)));
-#endif
-      feed.reset(new TailFeeder(c, fill, ud, len, feed_cut, fth, c->piece_seq));
-    }
     for (w = 0; w < nwin; ++w) {
       ws = w * W;
       wl = std::min(W, len - ws);
       uint8_t* buf = c->idx_win[w & 1].p;
+      bool feed_on = tail_on && w + 1 == nwin;
+#if DSX_DIAG
+      if (nwin > 1 && getenv("DSX_FEED_MULTI") && atoi(getenv("DSX_FEED_MULTI")) == 0) feed_on = false;
+#endif
+      if (feed_on) {
+        int fth = kFeedThreads;
+#if DSX_DIAG
+        if (const char* v = getenv("DSX_FEED_THREADS")) fth = std::max(1, std::min(64, atoi(v)));
+#endif
+        feed.reset(new TailFeeder(c, fill, ud, len, feed_cut, fth, c->piece_seq,
+                                  nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w));
+      }
       // the digest of window w-2 read this buffer; the copy stream waits for it
       if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
       if (w >= 1)  // the previous window's last `pre` bytes (it was a full window)
@@ -560,6 +591,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       }
       hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
                          (const DevState*)c->state.p, c->idx_snap.p + 2 * (w + 1));
+      if (tail_on && w + 2 == nwin) {  // (the last window's feeder starts from this snapshot)
+        hipError_t e = hipEventRecord(feed_ev.e, c->stream);
+        if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
+      }
       DigestArgs da{};
       da.blob = w == 0 ? buf + pre : buf;
       da.base_off = w == 0 ? 0 : ws - pre;

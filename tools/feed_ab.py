@@ -5,7 +5,7 @@ settings and `dsx_cut_fd` (the same read without IDs), the cases alternating
 call by call so that the box's drift in page-cache read speed falls on all of
 them alike.  Needs the diagnostic build for DSX_FEED_THREADS:
 
-  DSX_LIB_PATH=desync_amd/libdsx_diag.so python3 tools/feed_ab.py [rounds] [case ...]
+  DSX_LIB_PATH=desync_amd/libdsx_diag.so python3 tools/feed_ab.py [--gib=N] [rounds] [case ...]
 
 A case is name=THREADS:CUT[:READERS] (CUT -1 = the default, else
 DSX_INDEX_HOST_TAIL; READERS = DSX_INDEX_READERS, default 4) or `cut[:READERS]`
@@ -31,16 +31,20 @@ MIN, AVG, MAX = 16 << 10, 64 << 10, 256 << 10
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    cases = sys.argv[2:] or ["t11=11:-1", "t8=8:-1", "t11c96=11:98304", "off=11:0", "cut"]
-    n = 1 << 30
+    args = sys.argv[1:]
+    gib = 1
+    if args and args[0].startswith("--gib="):
+        gib = int(args.pop(0).split("=")[1])
+    rounds = int(args[0]) if args else 8
+    cases = args[1:] or ["t11=11:-1", "t8=8:-1", "t11c96=11:98304", "off=11:0", "cut"]
+    n = gib << 30
     rng = np.random.default_rng(7)
     fd, path = tempfile.mkstemp(prefix="dsx_feed_")
     res = {c.split("=")[0]: [] for c in cases}
     ratio = {c.split("=")[0]: [] for c in cases}
     try:
         with os.fdopen(fd, "wb") as f:
-            for _ in range(4):
+            for _ in range(4 * gib):
                 f.write(rng.integers(0, 256, 256 << 20, dtype=np.uint8).tobytes())
         # one context per cut (DSX_INDEX_HOST_TAIL is read when a context is
         # made; DSX_FEED_THREADS at each call): switching settings through the
@@ -76,6 +80,8 @@ def main():
                         desync_amd.ids_fd(fdr, 0, ends, ctx=ctxs[key(c)])
                     else:
                         os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
+                        # (a name ending in `_nomulti`: no feeder on the last of several windows)
+                        os.environ["DSX_FEED_MULTI"] = "0" if name.endswith("_nomulti") else "1"
                         t0 = time.perf_counter()
                         desync_amd.index_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
                     times[name] = time.perf_counter() - t0
@@ -96,7 +102,7 @@ def main():
         out[name] = {"gibs_median": round(float(np.median(v)), 2), "gibs_min": round(min(v), 2),
                      "gibs_max": round(max(v), 2),
                      "ratio_to_cut_fd_median": round(float(np.median(ratio[name])), 3) if ratio[name] else None}
-    print(json.dumps({"tool": "feed_ab", "gib": 1, "rounds": rounds, "cases": cases, "results": out}))
+    print(json.dumps({"tool": "feed_ab", "gib": gib, "rounds": rounds, "cases": cases, "results": out}))
 
 
 if __name__ == "__main__":
