@@ -773,9 +773,10 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   std::vector<TailChunk> tail;
   std::vector<uint8_t> tail_ids;
   c->stats.host_tail_chunks = 0;
-  // One window: the list is known up front, so the host hashes its long
-  // chunks from the start, beside the read (the tail feeder of run_index
-  // without the wait for the stitch); the digest skips them.
+  // The list is known up front, so the host hashes the last window's long
+  // chunks (all of them in one window) from the start, beside the read (the
+  // tail feeder of run_index without the wait for the stitch); that window's
+  // digest skips them.
   const uint64_t early_cut = c->index_host_tail > 0 ? (uint64_t)c->index_host_tail : kFeedCut;
   std::vector<TailChunk> early;
   std::vector<uint8_t> early_ids;
@@ -786,10 +787,11 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       if (t.joinable()) t.join();
     }
   } early_th;
-  if (tail_on && nwin == 1) {
+  if (tail_on) {
+    const uint64_t last_ws = (nwin - 1) * W;  // (the last window: chunks ending past it)
     for (uint64_t i = 0; i < n; ++i) {
       const uint64_t s0 = i ? ends[i - 1] - start : 0, e0 = ends[i] - start;
-      if (e0 - s0 > early_cut) early.push_back({i, s0, e0 - s0});
+      if ((nwin == 1 || e0 > last_ws) && e0 - s0 > early_cut) early.push_back({i, s0, e0 - s0});
     }
     std::sort(early.begin(), early.end(), [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
     early_ids.assign(32 * early.size(), 0);
@@ -836,8 +838,7 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       da.first_start = i0 == 0 ? 0 : ends[i0 - 1] - start;
       da.n = i1 - i0;
       da.ids = c->dg_ids.p + i0 * 32;
-      const int threads = (int)std::max(1u, std::min<unsigned>(kTailThreads, std::thread::hardware_concurrency()));
-      if (tail_on && w + 1 == nwin && nwin == 1) {
+      if (tail_on && w + 1 == nwin) {
         da.skip_above = early_cut;
         rc = launch_digest(c, da, i1 - i0, algo);
         if (rc) return drain(c, pf, rc);
@@ -851,19 +852,8 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
         i0 = i1;
         continue;
       }
-      if (tail_on && w + 1 == nwin) {
-        std::vector<uint64_t> rel(i1 - i0);
-        for (uint64_t i = i0; i < i1; ++i) rel[i - i0] = ends[i] - start;
-        tail = plan_tail(c, rel, i0, da.first_start, threads, &da.skip_above);
-      }
       rc = launch_digest(c, da, i1 - i0, algo);
       if (rc) return drain(c, pf, rc);
-      if (!tail.empty()) {  // the host's share while the GPU hashes the rest
-        tail_ids.assign(32 * tail.size(), 0);
-        rc = hash_tail(fill_shifted, &sh, tail, tail_ids.data(), threads);
-        if (rc) return drain(c, pf, rc);
-        c->stats.host_tail_chunks = tail.size();
-      }
     } else if (k >= 1) {  // (the window's buffer is free once its copies landed)
       hipError_t e = hipStreamWaitEvent(c->stream, c->idx_copy_ev[(k - 1) % K], 0);
       if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: wait"));
