@@ -647,6 +647,8 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
           continue;
         }
+        // (the end tail: reached only with the last-window feeder switched off,
+        // DSX_FEED_MULTI=0 in the diagnostic build, the comparison of r05bt)
         tail = plan_tail(c, ends, i0, snap[1], threads, &da.skip_above);
         rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
         if (rc) return drain(c, pf, rc);
