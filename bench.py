@@ -286,20 +286,33 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if args.gpus != world:
+        # a line for N GPUs must come from N ranks (the driver launches N > 1
+        # through torch.distributed.run with --nproc-per-node N)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: launch N > 1 "
+                         f"through torch.distributed.run --nproc-per-node {args.gpus}")
     # one GPU per rank; DSX_DIST_BACKEND=gloo with more ranks than GPUs is a
     # functional rehearsal of the N>1 path on a one-GPU box (not a measurement)
     backend = os.environ.get("DSX_DIST_BACKEND", "nccl")
     gpu = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     dist = None
+    ranks_counted = 1
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
+        # the ranks the collective backend itself sees (RCCL over xGMI for
+        # "nccl"): a sum of ones over the default group, before anything is
+        # timed, so that no curve point comes from fewer ranks than it claims
+        one = torch.ones(1, dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(one)
+        ranks_counted = int(one.item())
+        if int(one.item()) != world or dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: {backend} group has {int(one.item())} ranks "
+                             f"(world_size {dist.get_world_size()}), expected {world}")
     ctx = _lib.Context(gpu)
     n = int(args.gib * GiB)
     p = desync_amd.Params(MIN, AVG, MAX)
@@ -486,6 +499,7 @@ def main():
             "rank0": per_rank[0]["hbm"]}
         if dist:
             res["dist"] = dist_info(dist, backend, per_rank)
+            res["dist"]["ranks_counted_by_backend"] = ranks_counted
         if world == 1 and not args.no_cpu:
             # a bounded sample: the shard's first GiB (the leg is ~10-30 s of CPU work)
             host = blob[halo:halo + min(n, CPU_SAMPLE)].cpu().numpy()
