@@ -1139,8 +1139,10 @@ __global__ __launch_bounds__(W * kWave, W / 4) void scanl_kernel(ScanArgs a) {
       // (energy ablations, wrong results: 8 = no multiply (t = h), 9 = the 8 t
       // values OR-ed with full-rate v_bitop3 instead of the v_min3 tree, 10 =
       // 4-byte lookups, the ring takes T itself)
-      constexpr bool kTest = VARIANT == 0 || VARIANT == 4 || VARIANT == 5 || VARIANT == 7 ||
-                             VARIANT == 8 || VARIANT == 9 || VARIANT == 10;
+      // (VARIANT 6 hashes its trips in compute_il, but the handoff extension
+      // after them runs here and must test too: tests/test_gpu_variants.py)
+      constexpr bool kTest = VARIANT == 0 || VARIANT == 4 || VARIANT == 5 || VARIANT == 6 ||
+                             VARIANT == 7 || VARIANT == 8 || VARIANT == 9 || VARIANT == 10;
       uint32_t t[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
