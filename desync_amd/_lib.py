@@ -145,7 +145,7 @@ def _share_torch_hip_runtime():
 # "Environment"; tests/test_abi.py checks the library's strings against it).
 PRODUCT_ENV = ("DSX_TAIL_SPLIT", "DSX_LANE_TARGET", "DSX_SEG_FLOOR", "DSX_SCAN_NT",
                "DSX_DIGEST_PC", "DSX_DIGEST_LPT", "DSX_INDEX_WINDOW", "DSX_INDEX_SLOT",
-               "DSX_INDEX_READERS", "DSX_INDEX_HOST_TAIL")
+               "DSX_INDEX_READERS", "DSX_INDEX_HOST_TAIL", "DSX_HOST_THREADS")
 # Settings only libdsx_diag.so reads (scan ablations, other geometries,
 # rejected experiments), with the value the product library behaves as (None:
 # no such value).  Set to anything else with the product library they would
@@ -157,7 +157,8 @@ DIAG_ENV = {"DSX_SCAN_VARIANT": "0", "DSX_SCAN_CFG": "0", "DSX_FUSE": "0", "DSX_
             "DSX_DIGEST_PF": "1", "DSX_TAIL_MULT": "1", "DSX_LANE_BYTES": None,
             "DSX_STITCH_CUS": "0", "DSX_SCAN_MASK": "0", "DSX_SCAN_PRIO": None,
             "DSX_STREAM_BATCH": None, "DSX_NOOP_BEFORE_SCAN": None, "DSX_WALK_WGS": "2",
-            "DSX_WALK_NT": "576", "DSX_TAIL_LOG": None, "DSX_FEED_THREADS": None, "DSX_FEED_MULTI": None}
+            "DSX_WALK_NT": "576", "DSX_TAIL_LOG": None, "DSX_FEED_THREADS": None, "DSX_FEED_MULTI": None,
+            "DSX_FEED_MID": None}
 
 
 def lib():

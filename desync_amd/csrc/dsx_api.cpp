@@ -245,7 +245,9 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
     }
   }
 #endif
-  CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState)));
+  // coherent, like h_ring: the tail feeder (dsx_index.cpp) and dsx_progress
+  // poll it while the stitch publishes into it mid-call
+  CREATE_STEP(hipHostMalloc((void**)&c->h_state, sizeof(HostState), hipHostMallocCoherent));
   // coherent: dsx_result polls the seq the GPU publishes here
   CREATE_STEP(hipHostMalloc((void**)&c->h_ring, kQueueDepth * sizeof(HostState), hipHostMallocCoherent));
   memset(c->h_ring, 0, kQueueDepth * sizeof(HostState));
@@ -1356,8 +1358,11 @@ extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_
 // (the grid is sized from it; with da.range_lo the count is read on the
 // device).
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream,
-                  uint32_t* queue) {
-  const bool own = stream == nullptr;  // the ctx stream: launches run one after another
+                  uint32_t* queue, bool serial) {
+  // the ctx stream, or a stream whose digests the caller runs one after
+  // another (serial: dsx_index_*'s digest stream): the size-order scratch
+  // (dg_order, dg_cls) is then never used by two launches at once
+  const bool own = stream == nullptr || serial;
   if (!stream) stream = c->stream;
   if (!queue) {
     HIPCHK(c, c->dg_queue.ensure(1));

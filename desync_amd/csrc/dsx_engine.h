@@ -309,7 +309,12 @@ struct dsx_ctx {
   DevBuf<uint8_t> idx_win[2];
   DevBuf<uint64_t> idx_snap;
   hipEvent_t idx_copy_ev[kIdxSlots] = {};
-  hipEvent_t idx_win_ev[2] = {};
+  hipEvent_t idx_win_ev[2] = {};      // (recorded on idx_dg_stream after a window's digest)
+  hipEvent_t idx_stitch_ev[2] = {};   // a window's last stitch + snapshot (on stream)
+  // dsx_index_*'s digests run here, so a window's digest (its longest chunk's
+  // chain, ~10-15 ms) does not hold the next window's scans and stitches on
+  // `stream` (nor the tail feeder, which follows their published totals)
+  hipStream_t idx_dg_stream = nullptr;
   hipEvent_t q_ev[kQueueDepth] = {};
   uint32_t q_next = 0;
 };
@@ -363,6 +368,10 @@ int ensure_attr_walk(dsx_ctx* c);
 // host threads (dsx_stream.cpp): fn(0) on the caller, fn(1..parts-1) on a
 // persistent pool; returns when all have returned
 void host_parallel(int parts, const std::function<void(int)>& fn);
+// host CPUs this process may use (dsx_stream.cpp): the affinity mask, a
+// cgroup v2 quota and OMP_NUM_THREADS (the GPU box's per-GPU share), or
+// DSX_HOST_THREADS when set
+int host_cpu_share();
 // SHA-512/256 on the host (dsx_hostsha.cpp): one message, or 8 at once in
 // AVX-512 lanes (only when host_sha_vec(); n[i] == UINT64_MAX: unused lane)
 bool host_sha_vec();
@@ -385,6 +394,6 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
 // digest_kernel on `stream` (null: the ctx stream) with queue counter `queue`
 // (null: the ctx's); max_n bounds the chunk count (sizes the grid)
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream = nullptr,
-                  uint32_t* queue = nullptr);
+                  uint32_t* queue = nullptr, bool serial = false);
 void index_release(dsx_ctx* c);   // dsx_index.cpp: frees the pipeline's buffers
 void stream_release(dsx_ctx* c);  // dsx_stream.cpp: frees the stream's buffers

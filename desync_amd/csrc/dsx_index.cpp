@@ -163,6 +163,21 @@ int index_setup(dsx_ctx* c, uint64_t slot_bytes) {
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : c->idx_win_ev)
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : c->idx_stitch_ev)
+    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (!c->idx_dg_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->idx_dg_stream, hipStreamNonBlocking));
+  return DSX_OK;
+}
+
+// A window's digest on the digest stream, after the window's last stitch and
+// snapshot (recorded on `stream`); then the event the copy stream waits for
+// before it refills the window's buffer.
+int launch_window_digest(dsx_ctx* c, const DigestArgs& da, uint64_t max_n, int algo, int slot) {
+  HIPCHK(c, hipEventRecord(c->idx_stitch_ev[slot], c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->idx_dg_stream, c->idx_stitch_ev[slot], 0));
+  const int rc = launch_digest(c, da, max_n, algo, c->idx_dg_stream, nullptr, true);
+  if (rc) return rc;
+  HIPCHK(c, hipEventRecord(c->idx_win_ev[slot], c->idx_dg_stream));
   return DSX_OK;
 }
 
@@ -173,6 +188,7 @@ int drain(dsx_ctx* c, Prefetcher& pf, int rc) {
   (void)hipStreamSynchronize(c->copy_stream);
   (void)hipStreamSynchronize(c->scan_stream);
   (void)hipStreamSynchronize(c->stream);
+  if (c->idx_dg_stream) (void)hipStreamSynchronize(c->idx_dg_stream);
   return rc;
 }
 
@@ -201,6 +217,9 @@ struct ProgressScope {
 // runs at the clock an idle-ish GPU has then, ~58 ns per byte, against ~38 ns
 // on a busy one; 16 host threads read and hash ~43 GB/s)
 constexpr double kGpuNsPerByte = 58.0;   // digest_pc_kernel, one lane, end of a file call
+#if DSX_DIAG
+constexpr double kReadBytesPerNs = 45.0;  // page cache -> HBM through the pinned slots (dsx_cut_fd, ~42 GiB/s)
+#endif
 constexpr double kHostNsPerByte = 0.38;  // one host thread, read + hash (AVX-512)
 constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
 constexpr int kTailThreads = 16;
@@ -249,7 +268,11 @@ std::vector<TailChunk> plan_tail(const dsx_ctx* c, const std::vector<uint64_t>& 
 
 // Hashes the planned chunks (their bytes read again through `fill`) into
 // ids[32 j] for t[j]; 8 at a time per thread.
-int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* ids, int threads) {
+// Stops with DSX_E_INTERRUPTED between groups once `halt` (the caller's: a
+// feeder told to stop, an error path joining it) or `cancel` (dsx_cancel) is
+// set, so a cancelled call does not wait for a whole window's host hash.
+int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* ids, int threads,
+              const std::atomic<int>* halt, const std::atomic<int>* cancel) {
   const bool vec = host_sha_vec();
   const uint64_t per = vec ? 8 : 1;
   const uint64_t groups = (t.size() + per - 1) / per;
@@ -258,6 +281,11 @@ int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* i
   host_parallel((int)std::min<uint64_t>((uint64_t)threads, groups), [&](int) {
     std::vector<uint8_t> buf;
     for (uint64_t g; err.load() == DSX_OK && (g = next.fetch_add(1)) < groups;) {
+      if ((halt && halt->load(std::memory_order_relaxed)) ||
+          (cancel && cancel->load(std::memory_order_relaxed))) {
+        err.store(DSX_E_INTERRUPTED);
+        return;
+      }
       const uint64_t j0 = g * per, j1 = std::min<uint64_t>(t.size(), j0 + per);
       uint64_t total = 0;
       for (uint64_t j = j0; j < j1; ++j) total += t[j].len;
@@ -327,6 +355,7 @@ class TailFeeder {
     return err_;
   }
   void stop() {
+    halt_.store(1);  // (a batch being hashed ends at its next group of 8)
     {
       std::lock_guard<std::mutex> g(m_);
       stop_ = true;
@@ -402,7 +431,7 @@ class TailFeeder {
                     [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
           const size_t at = chunks.size();
           ids.resize(32 * (at + batch.size()));
-          const int rc = hash_tail(fill_, ud_, batch, ids.data() + 32 * at, threads_);
+          const int rc = hash_tail(fill_, ud_, batch, ids.data() + 32 * at, threads_, &halt_, &c_->cancel);
           if (rc) {
             err_ = rc;
             break;
@@ -427,17 +456,31 @@ class TailFeeder {
   std::mutex m_;
   std::condition_variable cv_;
   bool stop_ = false, have_final_ = false;
+  std::atomic<int> halt_{0};
   uint64_t final_ = 0;
   int err_ = DSX_OK;
 };
-// the GPU keeps chunks up to kFeedCut (a ~1.7 ms chain at the end); the host
-// the rest, ~87 % of the bytes, on kFeedThreads beside the 4 readers: more
-// threads than the box's 16-CPU share, but the host's rate is what bounds the
-// end (tools/feed_ab.py, profiles/r05bi-r05bp: 11 threads at 64 KiB 0.75-0.82 x
-// dsx_cut_fd, 24 at 32 KiB 0.78-0.89, 28 at 28 KiB 0.87-0.88; fewer threads,
-// 32 of them, or 40-48 KiB no better)
-constexpr uint64_t kFeedCut = 28ull << 10;
-constexpr int kFeedThreads = 28;
+// The host's share of the tail: feed_threads() SHA threads beside the
+// readers, within the process's CPU share (host_cpu_share: 16 on the GPU box,
+// whose affinity mask shows the whole machine); the GPU keeps the chunks up
+// to feed_cut() bytes (a 58 ns/B chain at the end of the call), the host the
+// longer ones.  Fewer threads hash less per ms, so the cut rises with them:
+// 28 KiB at 28 threads (round 5's setting, above the share), 64 KiB at 12
+// (tools/feed_ab.py).
+constexpr uint64_t kFeedCutBase = 28ull << 10;  // at kFeedThreadsBase threads
+constexpr int kFeedThreadsBase = 28;
+int feed_threads(const dsx_ctx* c) {
+  int t = std::max(1, host_cpu_share() - c->index_readers);
+#if DSX_DIAG
+  if (const char* v = getenv("DSX_FEED_THREADS")) t = std::max(1, std::min(64, atoi(v)));
+#endif
+  return t;
+}
+uint64_t feed_cut(const dsx_ctx* c, int threads) {
+  if (c->index_host_tail > 0) return (uint64_t)c->index_host_tail;  // forced (tests, A/B)
+  const uint64_t cut = kFeedCutBase * (uint64_t)kFeedThreadsBase / (uint64_t)std::max(1, threads);
+  return std::min<uint64_t>(128ull << 10, std::max<uint64_t>(kFeedCutBase, (cut + 2047) & ~4095ull));
+}
 
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
               uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {
@@ -463,7 +506,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   if (rc) return rc;
   HIPCHK(c, grow(c, c->idx_win[0], pre + W));
   if (nwin > 1) HIPCHK(c, grow(c, c->idx_win[1], pre + W));
-  HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 1)));
+  HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 2)));  // (+1: the one window's mid snapshot)
   HIPCHK(c, grow(c, c->out, need));
   if (algo >= 0) HIPCHK(c, grow(c, c->dg_ids, need * 32));
   const int K = dsx_ctx::kIdxSlots;
@@ -498,10 +541,11 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         da.ids = c->dg_ids.p;
         da.range_lo = c->idx_snap.p + 2 * w;
         da.range_hi = c->idx_snap.p + 2 * (w + 1);
-        if (launch_digest(c, da, (pre + wl) / p->min + 2, algo)) return err;
+        if (launch_window_digest(c, da, (pre + wl) / p->min + 2, algo, (int)(w & 1))) return err;
       }
       HostState st;
       (void)hipStreamSynchronize(c->stream);
+      (void)hipStreamSynchronize(c->idx_dg_stream);
       if (read_state(c, &st) || st.err) return err;  // (no piece stitched yet: nothing)
       const uint64_t n = std::min<uint64_t>(st.total, cap);
       if (n && hipMemcpy(out_ends, c->out.p, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return err;
@@ -525,9 +569,34 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         if (e) (void)hipEventDestroy(e);
       }
     } feed_ev;
-    if (tail_on && nwin > 1) HIPCHK(c, hipEventCreateWithFlags(&feed_ev.e, hipEventDisableTiming));
+    if (tail_on) HIPCHK(c, hipEventCreateWithFlags(&feed_ev.e, hipEventDisableTiming));
     std::unique_ptr<TailFeeder> feed;
-    const uint64_t feed_cut = c->index_host_tail > 0 ? (uint64_t)c->index_host_tail : kFeedCut;
+    const int fth = feed_threads(c);
+    const uint64_t fcut = feed_cut(c, fth);
+    // (Diagnostic) one window (a file up to DSX_INDEX_WINDOW): its first `mid` bytes are
+    // hashed on the GPU WHILE the rest is read -- a digest on the digest
+    // stream over the chunks stitched by then, every size (its chain, at most
+    // max bytes, ends before the read does) -- and the tail feeder starts at
+    // that point, so the host hashes only the long chunks after it.  mid is
+    // where the remaining read time covers the longest chain: (1 - mid/len)
+    // x the read time >= max x kGpuNsPerByte, at most half the window.  (The
+    // host, at the process's CPU share, cannot keep up with the long chunks
+    // of a whole window)
+    uint64_t mid_at = 0;
+#if DSX_DIAG
+    // (measured, not kept: the host, which then starts at mid, finished
+    // later -- 0.72 x dsx_cut_fd against 0.78 without, profiles/r06e; the
+    // diagnostic build keeps it behind DSX_FEED_MID for the record)
+    if (tail_on && nwin == 1 && getenv("DSX_FEED_MID")) {
+      const double t_read = (double)len / kReadBytesPerNs;     // ns
+      double frac = 1.0 - (double)p->max * kGpuNsPerByte / t_read;
+      frac = std::min(frac, 0.5);
+      frac = std::min(frac, atof(getenv("DSX_FEED_MID")));
+      if (frac >= 0.1) mid_at = (uint64_t)(frac * (double)len);
+    }
+#endif
+    uint64_t* const mid_snap = c->idx_snap.p + 2 * (nwin + 1);
+    bool mid_done = false;
     for (w = 0; w < nwin; ++w) {
       ws = w * W;
       wl = std::min(W, len - ws);
@@ -536,12 +605,8 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #if DSX_DIAG
       if (nwin > 1 && getenv("DSX_FEED_MULTI") && atoi(getenv("DSX_FEED_MULTI")) == 0) feed_on = false;
 #endif
-      if (feed_on) {
-        int fth = kFeedThreads;
-#if DSX_DIAG
-        if (const char* v = getenv("DSX_FEED_THREADS")) fth = std::max(1, std::min(64, atoi(v)));
-#endif
-        feed.reset(new TailFeeder(c, fill, ud, len, feed_cut, fth, c->piece_seq,
+      if (feed_on && !mid_at) {
+        feed.reset(new TailFeeder(c, fill, ud, len, fcut, fth, c->piece_seq,
                                   nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w));
       }
       // the digest of window w-2 read this buffer; the copy stream waits for it
@@ -575,6 +640,30 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           c->timing = true;
           if (rc) return drain(c, pf, rc);
           scanned = end;
+          if (mid_at && !mid_done && end >= mid_at && end < len) {
+            // the GPU's share of the one window: chunks [0, mid_snap.total)
+            mid_done = true;
+            hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
+                               (const DevState*)c->state.p, mid_snap);
+            e = hipEventRecord(feed_ev.e, c->stream);
+            if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
+            DigestArgs dm{};
+            dm.blob = buf + pre;
+            dm.base_off = 0;
+            dm.len = end;
+            dm.ends = c->out.p;
+            dm.ids = c->dg_ids.p;
+            dm.range_lo = c->idx_snap.p;
+            dm.range_hi = mid_snap;
+            rc = launch_window_digest(c, dm, end / p->min + 2, algo, 0);
+            if (rc) return drain(c, pf, rc);
+            feed.reset(new TailFeeder(c, fill, ud, len, fcut, fth, c->piece_seq, feed_ev.e, mid_snap));
+#if DSX_DIAG
+            if (getenv("DSX_TAIL_LOG"))
+              fprintf(stderr, "index: GPU share of the window up to %.1f MB, %.2f ms into the call\n",
+                      end / 1e6, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
+#endif
+          }
 #if DSX_DIAG
           if (end == len && getenv("DSX_TAIL_LOG"))
             fprintf(stderr, "index: last piece enqueued %.2f ms into the call\n",
@@ -601,7 +690,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       da.len = w == 0 ? wl : pre + wl;
       da.ends = c->out.p;
       da.ids = c->dg_ids.p;
-      da.range_lo = c->idx_snap.p + 2 * w;
+      da.range_lo = mid_done ? mid_snap : c->idx_snap.p + 2 * w;  // (after the GPU's share)
       da.range_hi = c->idx_snap.p + 2 * (w + 1);
       if (tail_on && w + 1 == nwin) {
         // the window's chunk ends (the stitch is done once the stream is)
@@ -615,10 +704,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         if (i1 > i0)
           e = hipMemcpy(ends.data(), c->out.p + i0, (i1 - i0) * 8, hipMemcpyDeviceToHost);
         if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: tail ends"));
-        const int threads = (int)std::max(1u, std::min<unsigned>(kTailThreads, std::thread::hardware_concurrency()));
+        const int threads = std::max(1, std::min(kTailThreads, host_cpu_share()));
         if (feed) {  // the feeder has the long chunks: the GPU the rest
-          da.skip_above = feed_cut;
-          rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
+          da.skip_above = fcut;
+          rc = launch_window_digest(c, da, (pre + wl) / p->min + 2, algo, (int)(w & 1));
           if (rc) return drain(c, pf, rc);
 #if DSX_DIAG
           const auto tf0 = std::chrono::steady_clock::now();
@@ -628,6 +717,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #endif
           feed->finish(i1);
           rc = feed->join();
+          if (rc == DSX_E_INTERRUPTED) return partial(rc);  // (dsx_cancel during the host hash)
           if (rc) return drain(c, pf, rc);
           tail = std::move(feed->chunks);
           tail_ids = std::move(feed->ids);
@@ -636,28 +726,26 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           if (getenv("DSX_TAIL_LOG")) {
             const double hms =
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
-            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->idx_dg_stream);
             const double gms =
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
             fprintf(stderr, "feed: chunks %lu host %zu (cut %lu) host done %.2f ms, GPU done %.2f ms\n",
-                    (unsigned long)i1, tail.size(), (unsigned long)feed_cut, hms, gms);
+                    (unsigned long)i1, tail.size(), (unsigned long)fcut, hms, gms);
           }
 #endif
-          e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
-          if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
           continue;
         }
         // (the end tail: reached only with the last-window feeder switched off,
         // DSX_FEED_MULTI=0 in the diagnostic build, the comparison of r05bt)
         tail = plan_tail(c, ends, i0, snap[1], threads, &da.skip_above);
-        rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
+        rc = launch_window_digest(c, da, (pre + wl) / p->min + 2, algo, (int)(w & 1));
         if (rc) return drain(c, pf, rc);
         // the host's share while the GPU hashes the rest
         tail_ids.assign(32 * tail.size(), 0);
 #if DSX_DIAG
         const auto th0 = std::chrono::steady_clock::now();
 #endif
-        if (!tail.empty()) rc = hash_tail(fill, ud, tail, tail_ids.data(), threads);
+        if (!tail.empty()) rc = hash_tail(fill, ud, tail, tail_ids.data(), threads, nullptr, &c->cancel);
         if (rc) return drain(c, pf, rc);
         c->stats.host_tail_chunks = tail.size();
 #if DSX_DIAG
@@ -665,23 +753,22 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           uint64_t hb = 0;
           for (const auto& x : tail) hb += x.len;
           const double hms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
-          (void)hipStreamSynchronize(c->stream);
+          (void)hipStreamSynchronize(c->idx_dg_stream);
           const double gms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
           fprintf(stderr, "tail: window chunks %lu host %zu (%.1f MB, cut %lu) host %.2f ms, GPU done %.2f ms\n",
                   (unsigned long)ends.size(), tail.size(), hb / 1e6, (unsigned long)da.skip_above, hms, gms);
         }
 #endif
       } else {
-        rc = launch_digest(c, da, (pre + wl) / p->min + 2, algo);
+        rc = launch_window_digest(c, da, (pre + wl) / p->min + 2, algo, (int)(w & 1));
         if (rc) return drain(c, pf, rc);
       }
-      hipError_t e = hipEventRecord(c->idx_win_ev[w & 1], c->stream);
-      if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
     }
     pf.stop();
     HostState st;
-    rc = read_state(c, &st);  // waits for the last digest too (same stream)
+    rc = read_state(c, &st);  // (the stitches)
     HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+    HIPCHK(c, hipStreamSynchronize(c->idx_dg_stream));  // (the digests)
     if (rc) return rc;
     if (st.err & kErrDense) {  // rare: a lane overflowed its candidate slots
       c->stats.dense_fallbacks++;
@@ -767,6 +854,14 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
     return s->fill(s->ud, dst, s->start + off, cnt);
   };
   const int K = dsx_ctx::kIdxSlots;
+#if DSX_DIAG
+  // (DSX_TAIL_LOG: the call's phases, to find which one a slow call spends
+  // its time in -- the reads, the wait for the early host hash, the GPU)
+  const bool tlog = getenv("DSX_TAIL_LOG") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  double t_read = 0, t_join0 = 0, t_join1 = 0;
+#endif
   Prefetcher pf(fill_shifted, &sh, L, piece, c->idx_slots, K, c->index_readers);
   uint64_t k = 0, i0 = 0;
   // the host tail of the last window, as in run_index (the list is known here)
@@ -779,13 +874,16 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   // chunks (all of them in one window) from the start, beside the read (the
   // tail feeder of run_index without the wait for the stitch); that window's
   // digest skips them.
-  const uint64_t early_cut = c->index_host_tail > 0 ? (uint64_t)c->index_host_tail : kFeedCut;
+  const int eth = feed_threads(c);
+  const uint64_t early_cut = feed_cut(c, eth);
   std::vector<TailChunk> early;
   std::vector<uint8_t> early_ids;
   int early_rc = DSX_OK;
-  struct Joiner {
+  struct Joiner {  // (an error return stops the early hash at its next group, then joins)
     std::thread t;
+    std::atomic<int> halt{0};
     ~Joiner() {
+      halt.store(1);
       if (t.joinable()) t.join();
     }
   } early_th;
@@ -797,12 +895,10 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
     }
     std::sort(early.begin(), early.end(), [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
     early_ids.assign(32 * early.size(), 0);
-    int eth = kFeedThreads;
-#if DSX_DIAG
-    if (const char* v = getenv("DSX_FEED_THREADS")) eth = std::max(1, std::min(64, atoi(v)));
-#endif
     if (!early.empty())
-      early_th.t = std::thread([&, eth] { early_rc = hash_tail(fill_shifted, &sh, early, early_ids.data(), eth); });
+      early_th.t = std::thread([&, eth] {
+        early_rc = hash_tail(fill_shifted, &sh, early, early_ids.data(), eth, &early_th.halt, &c->cancel);
+      });
   }
   for (uint64_t w = 0; w < nwin; ++w) {
     const uint64_t ws = w * W, wl = std::min(W, L - ws);
@@ -844,7 +940,13 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
         da.skip_above = early_cut;
         rc = launch_digest(c, da, i1 - i0, algo);
         if (rc) return drain(c, pf, rc);
+#if DSX_DIAG
+        t_read = t_join0 = ms();
+#endif
         if (early_th.t.joinable()) early_th.t.join();
+#if DSX_DIAG
+        t_join1 = ms();
+#endif
         if (early_rc) return drain(c, pf, early_rc);
         tail = std::move(early);
         tail_ids = std::move(early_ids);
@@ -868,6 +970,16 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   HIPCHK(c, hipStreamSynchronize(c->copy_stream));
   HIPCHK(c, hipMemcpyAsync(out_ids, c->dg_ids.p, n * 32, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+#if DSX_DIAG
+  if (tlog) {
+    uint64_t hb = 0;
+    for (const auto& x : tail) hb += x.len;
+    fprintf(stderr, "ids: %.1f MB windows %lu reads+H2D done %.2f ms, early hash joined %.2f ms "
+            "(waited %.2f; %zu chunks %.1f MB on %d threads, cut %lu), GPU done %.2f ms\n",
+            L / 1e6, (unsigned long)nwin, t_read, t_join1, t_join1 - t_join0, tail.size(), hb / 1e6, eth,
+            (unsigned long)early_cut, ms());
+  }
+#endif
   for (size_t j = 0; j < tail.size(); ++j)  // (the GPU skipped these)
     memcpy(out_ids + 32 * tail[j].idx, tail_ids.data() + 32 * j, 32);
   return DSX_OK;
@@ -876,6 +988,13 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
 }  // namespace
 
 void index_release(dsx_ctx* c) {
+  if (c->idx_dg_stream) {
+    (void)hipStreamSynchronize(c->idx_dg_stream);
+    (void)hipStreamDestroy(c->idx_dg_stream);
+    c->idx_dg_stream = nullptr;
+  }
+  for (auto& e : c->idx_stitch_ev)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
   for (auto& s : c->idx_slots) {
     if (s) (void)hipHostFree(s);
     s = nullptr;

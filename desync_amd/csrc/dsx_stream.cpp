@@ -15,9 +15,12 @@
 // Popped chunk bytes alias the host buffer until the next call (Next's rule,
 // chunker.go:202-205).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -657,6 +660,37 @@ class HostPool {
   const std::function<void(int)>* fn_ = nullptr;
 };
 }  // namespace
+
+int host_cpu_share() {
+  const int share = [] {
+    if (const char* v = getenv("DSX_HOST_THREADS")) {
+      const int o = atoi(v);
+      if (o > 0) return std::min(o, 256);
+    }
+    int n = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // "quota period" or "max period"
+      char q[32] = {0};
+      long long period = 0;
+      if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+        const long long quota = atoll(q);
+        if (quota > 0) n = (int)std::min<long long>(n, std::max(1LL, (quota + period - 1) / period));
+      }
+      fclose(f);
+    }
+    // (the GPU box exports its CPU share per GPU here; its affinity mask and
+    // nproc show the whole machine)
+    if (const char* v = getenv("OMP_NUM_THREADS")) {
+      const int o = atoi(v);
+      if (o > 0) n = std::min(n, o);
+    }
+    return std::max(1, n);
+  }();
+  return share;
+}
 
 void host_parallel(int parts, const std::function<void(int)>& fn) {
   if (parts <= 1) {

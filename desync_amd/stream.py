@@ -26,7 +26,10 @@ from .index import CaFormatExcludeNoDump, CaFormatSHA512256, ChunkArray, FormatI
 class Chunk:
     """chunk.go's Chunk, reduced to what a store needs: the ID and the
     uncompressed bytes.  ChunkStream's chunks hold a read-only view of the
-    clone of their run's bytes (bytes(chunk.Data()) copies it out)."""
+    clone of their run's bytes (bytes(chunk.Data()) copies it out).  The
+    store contract: the view is valid for as long as it is referenced, but it
+    pins the whole pooled slab (8 MiB) or run behind it, so a store that
+    keeps chunk bytes past StoreChunk copies them (MemoryStore does)."""
 
     __slots__ = ("_id", "_data")
 
@@ -95,8 +98,12 @@ class MemoryStore:
             return cid in self.chunks
 
     def StoreChunk(self, chunk: Chunk):
+        # Chunk.Data() is a read-only view into ChunkStream's pooled slab (or
+        # a whole run): a store that keeps the bytes takes its own copy, as
+        # Go's Chunk owns its []byte, so one kept chunk does not pin the slab
+        data = bytes(chunk.Data())
         with self._lock:
-            self.chunks[chunk.ID()] = chunk.Data()
+            self.chunks[chunk.ID()] = data
 
 
 _BATCH = 64  # chunks per hand-off to the store workers

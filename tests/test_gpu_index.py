@@ -102,6 +102,40 @@ def test_index_fd_reader_threads(tmp_path, monkeypatch, readers):
     assert [bytes(x) for x in ids] == _ids(data, ref, "sha512-256")
 
 
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_index_host_threads(tmp_path, monkeypatch, threads):
+    """DSX_HOST_THREADS caps the host threads (the tail feeder gets this less
+    the readers, at least one, and a higher cut); IDs stay hashlib's over
+    several windows and over one."""
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_HOST_THREADS", threads)
+    data = o.synth_uniform(44, 0, (12 << 20) + 777)
+    f = tmp_path / "blob"
+    f.write_bytes(data.tobytes())
+    ref = o.chunk_stream(data, MIN, AVG, MAX)
+    for window in (4 << 20, 64 << 20):
+        monkeypatch.setenv("DSX_INDEX_WINDOW", str(window))
+        ctx = _lib.Context(0)
+        try:
+            fd = os.open(str(f), os.O_RDONLY)
+            try:
+                ends, ids = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+            finally:
+                os.close(fd)
+            n_host = ctx.stats().host_tail_chunks
+        finally:
+            ctx.close()
+        assert np.array_equal(ends, ref)
+        assert [bytes(x) for x in ids] == _ids(data, ref, "sha512-256")
+        avx512 = "avx512f" in open("/proc/cpuinfo").read() and "avx512bw" in open("/proc/cpuinfo").read()
+        if window > data.size and avx512:
+            # one window: one feeder thread (1 or 3 host threads less the 4
+            # readers) and the cut 28 KiB x 28 / 1 capped at 128 KiB
+            lens = np.diff(np.concatenate([[0], ref.astype(np.int64)]))
+            assert n_host == int(np.sum(lens > 131072))
+
+
 @pytest.mark.parametrize("tail,window", [("65536", 16 << 20), ("0", 16 << 20), ("-1", 16 << 20),
                                          ("100000", None), ("-1", None)])
 def test_index_host_tail(tmp_path, monkeypatch, tail, window):
@@ -117,6 +151,9 @@ def test_index_host_tail(tmp_path, monkeypatch, tail, window):
     import desync_amd
     from desync_amd import _lib
     monkeypatch.setenv("DSX_INDEX_HOST_TAIL", tail)
+    # the default cut follows the feeder's threads (the CPU share less the 4
+    # readers): 32 host threads -> 28 feeders -> 28 KiB, independent of the box
+    monkeypatch.setenv("DSX_HOST_THREADS", "32")
     if window:
         monkeypatch.setenv("DSX_INDEX_WINDOW", str(window))
     data = o.synth_uniform(47, 0, (40 << 20) + 777)

@@ -46,6 +46,10 @@ def main():
         with os.fdopen(fd, "wb") as f:
             for _ in range(4 * gib):
                 f.write(rng.integers(0, 256, 256 << 20, dtype=np.uint8).tobytes())
+            # written back before timing: dirty pages flushed in the background
+            # during the timed calls slow the reads (round 6, tools/window_dip.py)
+            f.flush()
+            os.fsync(f.fileno())
         # one context per cut (DSX_INDEX_HOST_TAIL is read when a context is
         # made; DSX_FEED_THREADS at each call): switching settings through the
         # pool would close and remake them
@@ -82,6 +86,12 @@ def main():
                         os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
                         # (a name ending in `_nomulti`: no feeder on the last of several windows)
                         os.environ["DSX_FEED_MULTI"] = "0" if name.endswith("_nomulti") else "1"
+                        # (a name ending in `_mid`: the GPU's share of a one-window
+                        # file, DSX_FEED_MID=0.5 in the diagnostic build)
+                        if name.endswith("_mid"):
+                            os.environ["DSX_FEED_MID"] = "0.5"
+                        else:
+                            os.environ.pop("DSX_FEED_MID", None)
                         t0 = time.perf_counter()
                         desync_amd.index_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
                     times[name] = time.perf_counter() - t0

@@ -42,6 +42,8 @@ def main():
                     k = min(left, 256 << 20)
                     f.write(rng.integers(0, 256, k, dtype=np.uint8).tobytes())
                     left -= k
+                f.flush()
+                os.fsync(f.fileno())  # (no writeback during the timed calls)
             def make():
                 index, stats = desync_amd.IndexFromFile(None, path, 1, MIN, AVG, MAX)
                 b = io.BytesIO()
