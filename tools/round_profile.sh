@@ -34,7 +34,7 @@ for w in dedup zeros; do
   echo "$w: $(cat $OUT/bench_$w.json)"
 done
 timeout -k 10 400 python3 tools/digest_rate.py 1 4 16 > $OUT/digest_rate.json 2> $OUT/digest_rate.err || { tail $OUT/digest_rate.err; exit 1; }
-timeout -k 10 600 python3 tools/make_rate.py 1 4 > $OUT/make_rate.json 2> $OUT/make_rate.err || { tail $OUT/make_rate.err; exit 1; }
+timeout -k 10 600 python3 tools/make_rate.py 1 2 4 > $OUT/make_rate.json 2> $OUT/make_rate.err || { tail $OUT/make_rate.err; exit 1; }
 timeout -k 10 300 python3 tools/stream_rate.py > $OUT/stream_rate.json 2> $OUT/stream_rate.err || { tail $OUT/stream_rate.err; exit 1; }
 timeout -k 10 600 python3 tools/ab.py --rounds 3 $OUT/avg 'a16:+--avg=16' 'a64:+--avg=64' 'a256:+--avg=256' > $OUT/avg_sweep.txt 2>&1 || { tail $OUT/avg_sweep.txt; exit 1; }
 grep "^==" $OUT/avg_sweep.txt
