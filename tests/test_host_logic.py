@@ -82,6 +82,20 @@ def test_chunk_storage_dedup_and_retry():
     assert ws2.chunks == {b"b" * 32: b"y"}
 
 
+def test_memory_store_keeps_its_own_bytes():
+    """A store that keeps chunk bytes copies them (ChunkStream's Chunk.Data()
+    is a read-only view into a pooled slab; keeping the view would pin the
+    whole slab and change under a reused slab)."""
+    from desync_amd.stream import Chunk, MemoryStore
+
+    slab = bytearray(b"abcdefgh" * 4)
+    ws = MemoryStore()
+    ws.StoreChunk(Chunk(b"i" * 32, memoryview(slab)[8:16].toreadonly()))
+    slab[8:16] = b"XXXXXXXX"  # the slab is reused
+    got = ws.chunks[b"i" * 32]
+    assert isinstance(got, bytes) and got == b"abcdefgh"
+
+
 def test_legacy_hash_type():
     """chunker.go:320-371 (NewHash / Initialize / Roll / IsBoundary / Reset):
     after Initialize on a 48-byte window and Roll over the following bytes,
