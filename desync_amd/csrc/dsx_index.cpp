@@ -268,11 +268,26 @@ std::vector<TailChunk> plan_tail(const dsx_ctx* c, const std::vector<uint64_t>& 
 
 // Hashes the planned chunks (their bytes read again through `fill`) into
 // ids[32 j] for t[j]; 8 at a time per thread.
+// Where the host tail takes a chunk's bytes: straight from the caller's
+// memory (dsx_*_host), else read again through the call's fill function
+// (dsx_*_fd: the pages the readers just brought into the page cache).
+// (Taking them from the pinned read slots instead, each slot kept three
+// pieces longer for the feeder, saved the copy of ~0.7 GB per GiB and
+// measured no gain, in-process A/B at three cuts, profiles/r06n/: the SHA
+// rounds, not the copy, hold the host threads.)
+struct TailSrc {
+  FillFn fill;
+  void* ud;
+  const uint8_t* direct = nullptr;  // the source's bytes [0, len) in host memory
+};
+
 // Stops with DSX_E_INTERRUPTED between groups once `halt` (the caller's: a
 // feeder told to stop, an error path joining it) or `cancel` (dsx_cancel) is
 // set, so a cancelled call does not wait for a whole window's host hash.
-int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* ids, int threads,
+int hash_tail(const TailSrc& src, const std::vector<TailChunk>& t, uint8_t* ids, int threads,
               const std::atomic<int>* halt, const std::atomic<int>* cancel) {
+  const FillFn fill = src.fill;
+  void* const ud = src.ud;
   const bool vec = host_sha_vec();
   const uint64_t per = vec ? 8 : 1;
   const uint64_t groups = (t.size() + per - 1) / per;
@@ -294,6 +309,7 @@ int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* i
       uint64_t n[8];
       uint8_t* o[8];
       uint64_t at = 0;
+      int rc = DSX_OK;
       for (uint64_t j = j0; j < j0 + per; ++j) {
         const int q = (int)(j - j0);
         if (j >= j1) {
@@ -302,22 +318,26 @@ int hash_tail(FillFn fill, void* ud, const std::vector<TailChunk>& t, uint8_t* i
           o[q] = nullptr;
           continue;
         }
-        if (t[j].len) {
-          const int rc = fill(ud, buf.data() + at, t[j].start, t[j].len);
-          if (rc) {
-            err.store(rc);
-            return;
-          }
-        }
-        p[q] = buf.data() + at;
         n[q] = t[j].len;
         o[q] = ids + 32 * j;
+        if (src.direct) {
+          p[q] = src.direct + t[j].start;
+          continue;
+        }
+        if (t[j].len && rc == DSX_OK) rc = fill(ud, buf.data() + at, t[j].start, t[j].len);
+        p[q] = buf.data() + at;
         at += t[j].len;
       }
-      if (vec)
-        host_sha512_256_x8(p, n, o);
-      else
-        host_sha512_256_one(p[0], n[0], o[0]);
+      if (rc == DSX_OK) {
+        if (vec)
+          host_sha512_256_x8(p, n, o);
+        else
+          host_sha512_256_one(p[0], n[0], o[0]);
+      }
+      if (rc) {
+        err.store(rc);
+        return;
+      }
     }
   });
   return err.load();
@@ -334,9 +354,9 @@ class TailFeeder {
  public:
   // (the last of several windows: start_ev marks the previous window's
   // snapshot dsnap = {cuts before this window, their last end})
-  TailFeeder(dsx_ctx* c, FillFn fill, void* ud, uint64_t len, uint64_t cut, int threads,
+  TailFeeder(dsx_ctx* c, const TailSrc& src, uint64_t len, uint64_t cut, int threads,
              uint64_t seq0, hipEvent_t start_ev = nullptr, const uint64_t* dsnap = nullptr)
-      : c_(c), fill_(fill), ud_(ud), len_(len), cut_(cut), threads_(threads), seq0_(seq0),
+      : c_(c), src_(src), len_(len), cut_(cut), threads_(threads), seq0_(seq0),
         start_ev_(start_ev), dsnap_(dsnap) {
     th_ = std::thread([this] { run(); });
   }
@@ -431,7 +451,7 @@ class TailFeeder {
                     [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
           const size_t at = chunks.size();
           ids.resize(32 * (at + batch.size()));
-          const int rc = hash_tail(fill_, ud_, batch, ids.data() + 32 * at, threads_, &halt_, &c_->cancel);
+          const int rc = hash_tail(src_, batch, ids.data() + 32 * at, threads_, &halt_, &c_->cancel);
           if (rc) {
             err_ = rc;
             break;
@@ -444,8 +464,7 @@ class TailFeeder {
     (void)hipStreamDestroy(s);
   }
   dsx_ctx* c_;
-  FillFn fill_;
-  void* ud_;
+  TailSrc src_;
   uint64_t len_;
   uint64_t cut_;
   int threads_;
@@ -483,7 +502,8 @@ uint64_t feed_cut(const dsx_ctx* c, int threads) {
 }
 
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
-              uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out) {
+              uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out,
+              const uint8_t* direct = nullptr) {
   HIPCHK(c, hipSetDevice(c->device));
   c->err.clear();
   int rc = ensure_attr_walk(c);
@@ -521,6 +541,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->idx_snap.p, 0, 2 * sizeof(uint64_t), c->stream));  // {0 cuts, cut 0}
     Prefetcher pf(fill, ud, len, piece, c->idx_slots, K, c->index_readers);
+    const TailSrc tsrc{fill, ud, direct};  // (the host tail's bytes)
     uint64_t k = 0;  // piece index
     uint64_t w = 0, ws = 0, wl = 0;
     // Interrupted{} or a read error (make.go:133-162, :201-203): the chunks
@@ -606,7 +627,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       if (nwin > 1 && getenv("DSX_FEED_MULTI") && atoi(getenv("DSX_FEED_MULTI")) == 0) feed_on = false;
 #endif
       if (feed_on && !mid_at) {
-        feed.reset(new TailFeeder(c, fill, ud, len, fcut, fth, c->piece_seq,
+        feed.reset(new TailFeeder(c, tsrc, len, fcut, fth, c->piece_seq,
                                   nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w));
       }
       // the digest of window w-2 read this buffer; the copy stream waits for it
@@ -657,7 +678,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
             dm.range_hi = mid_snap;
             rc = launch_window_digest(c, dm, end / p->min + 2, algo, 0);
             if (rc) return drain(c, pf, rc);
-            feed.reset(new TailFeeder(c, fill, ud, len, fcut, fth, c->piece_seq, feed_ev.e, mid_snap));
+            feed.reset(new TailFeeder(c, tsrc, len, fcut, fth, c->piece_seq, feed_ev.e, mid_snap));
 #if DSX_DIAG
             if (getenv("DSX_TAIL_LOG"))
               fprintf(stderr, "index: GPU share of the window up to %.1f MB, %.2f ms into the call\n",
@@ -745,7 +766,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #if DSX_DIAG
         const auto th0 = std::chrono::steady_clock::now();
 #endif
-        if (!tail.empty()) rc = hash_tail(fill, ud, tail, tail_ids.data(), threads, nullptr, &c->cancel);
+        if (!tail.empty()) rc = hash_tail(tsrc, tail, tail_ids.data(), threads, nullptr, &c->cancel);
         if (rc) return drain(c, pf, rc);
         c->stats.host_tail_chunks = tail.size();
 #if DSX_DIAG
@@ -808,7 +829,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 // window where it ends, with all its bytes resident.  The ranges per window
 // come from the host's list (no device snapshots).
 int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t start,
-            const uint64_t* ends, uint64_t n, uint8_t* out_ids) {
+            const uint64_t* ends, uint64_t n, uint8_t* out_ids, const uint8_t* direct = nullptr) {
   HIPCHK(c, hipSetDevice(c->device));
   c->err.clear();
   if (n == 0) return DSX_OK;
@@ -897,7 +918,8 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
     early_ids.assign(32 * early.size(), 0);
     if (!early.empty())
       early_th.t = std::thread([&, eth] {
-        early_rc = hash_tail(fill_shifted, &sh, early, early_ids.data(), eth, &early_th.halt, &c->cancel);
+        const TailSrc esrc{fill_shifted, &sh, direct ? direct + start : nullptr};
+        early_rc = hash_tail(esrc, early, early_ids.data(), eth, &early_th.halt, &c->cancel);
       });
   }
   for (uint64_t w = 0; w < nwin; ++w) {
@@ -1064,7 +1086,7 @@ extern "C" int dsx_index_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, co
   if (!c || !p || !n_out || (len && !h_blob) || (cap && (!out_ends || !ids)) || bad_algo(algo))
     return DSX_E_INVAL;
   MemSrc s{(const uint8_t*)h_blob};
-  const int rc = run_index(c, p, algo, len, fill_mem, &s, out_ends, ids, cap, n_out);
+  const int rc = run_index(c, p, algo, len, fill_mem, &s, out_ends, ids, cap, n_out, s.p);
   c->cancel.store(0);
   return rc;
 }
@@ -1092,7 +1114,7 @@ extern "C" int dsx_ids_host(dsx_ctx_t* c, const void* h_blob, uint64_t len, uint
   DSX_FLUSH_BEHIND(c);
   if (!c || (len && !h_blob) || (n && (!ends || !ids)) || bad_algo(algo)) return DSX_E_INVAL;
   MemSrc s{(const uint8_t*)h_blob};
-  const int rc = run_ids(c, algo, len, fill_mem, &s, start, ends, n, ids);
+  const int rc = run_ids(c, algo, len, fill_mem, &s, start, ends, n, ids, s.p);
   c->cancel.store(0);
   return rc;
 }
