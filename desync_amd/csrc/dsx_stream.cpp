@@ -680,6 +680,16 @@ int host_cpu_share() {
         if (quota > 0) n = (int)std::min<long long>(n, std::max(1LL, (quota + period - 1) / period));
       }
       fclose(f);
+    } else if (FILE* fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // cgroup v1
+      long long quota = -1, period = 0;
+      if (fscanf(fq, "%lld", &quota) != 1) quota = -1;
+      fclose(fq);
+      if (FILE* fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+        if (fscanf(fp, "%lld", &period) != 1) period = 0;
+        fclose(fp);
+      }
+      if (quota > 0 && period > 0)
+        n = (int)std::min<long long>(n, std::max(1LL, (quota + period - 1) / period));
     }
     // (the GPU box exports its CPU share per GPU here; its affinity mask and
     // nproc show the whole machine)
