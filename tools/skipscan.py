@@ -74,9 +74,16 @@ def main():
     args = ap.parse_args()
     import torch
 
+    import subprocess
+
     import desync_amd
     from desync_amd import _lib
-    sk = ctypes.CDLL(os.path.join(REPO, "tools", "libskipscan.so"))
+    so = os.path.join(REPO, "tools", "libskipscan.so")
+    src = os.path.join(REPO, "tools", "skipscan.hip")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                               "-shared", "-fPIC", src, "-o", so])
+    sk = ctypes.CDLL(so)
     sk.skipscan_run.restype = ctypes.c_int
     L = _lib.lib()
     ctx = _lib.Context(0)
