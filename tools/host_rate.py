@@ -42,8 +42,13 @@ def main():
     data = t.cpu().numpy()
     del t
     st_host, ends_h = repeat(lambda: make.cut_host(data, MIN, AVG, MAX), n)
+    # cuts + SHA-512/256 IDs from host memory (the host tail hashes the
+    # caller's bytes in place)
+    st_ihost, _ = repeat(lambda: make.index_host(data, MIN, AVG, MAX), n)
     with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp"), delete=False) as f:
         data.tofile(f)
+        f.flush()
+        os.fsync(f.fileno())  # (no write-back under the timed calls)
         path = f.name
     try:
         fd = os.open(path, os.O_RDONLY)
@@ -58,6 +63,8 @@ def main():
         "bytes": n,
         "chunks": int(len(ends_h)),
         "cut_host_gibs": st_host["gibs_median"],
+        "index_host_gibs": st_ihost["gibs_median"],
+        "index_host": st_ihost,
         "cut_fd_gibs": st_fd["gibs_median"],
         "cut_host": st_host,
         "cut_fd": st_fd,
