@@ -64,3 +64,16 @@ def test_cpu_leg_matches_the_sequential_chain():
     blob = o.synth_uniform_c(2, 0, 8 << 20)
     assert np.array_equal(o.chunk_parallel(blob, bench.MIN, bench.AVG, bench.MAX, 4),
                           o.chunk_stream(blob, bench.MIN, bench.AVG, bench.MAX))
+
+
+def test_refuses_a_gpu_count_other_than_the_world_size():
+    """A line for N GPUs must come from N ranks: `--gpus 2` without
+    torch.distributed.run (WORLD_SIZE unset) stops before anything runs."""
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--no-cpu"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE 1" in r.stderr, r.stderr[-2000:]
+    assert not r.stdout.strip()

@@ -125,6 +125,7 @@ def test_bench_two_ranks_gloo_check():
     # rank's in-kernel scan stamps, every rank's HBM footprint
     assert line["dist"]["backend"] == "gloo" and line["dist"]["world_size"] == 2
     assert line["dist"]["ranks_reporting"] == 2
+    assert line["dist"]["ranks_counted_by_backend"] == 2
     rl = line["roofline"]
     assert len(rl["per_rank"]) == 2 and all(x["launches"] >= 3 for x in rl["per_rank"])
     assert rl["frac"] == min(x["frac"] for x in rl["per_rank"]) > 0
