@@ -394,6 +394,6 @@ int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t 
 // digest_kernel on `stream` (null: the ctx stream) with queue counter `queue`
 // (null: the ctx's); max_n bounds the chunk count (sizes the grid)
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream = nullptr,
-                  uint32_t* queue = nullptr, bool serial = false);
+                  uint32_t* queue = nullptr, bool serial = false, uint32_t max_blocks = 0);
 void index_release(dsx_ctx* c);   // dsx_index.cpp: frees the pipeline's buffers
 void stream_release(dsx_ctx* c);  // dsx_stream.cpp: frees the stream's buffers

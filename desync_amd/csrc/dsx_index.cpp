@@ -172,10 +172,11 @@ int index_setup(dsx_ctx* c, uint64_t slot_bytes) {
 // A window's digest on the digest stream, after the window's last stitch and
 // snapshot (recorded on `stream`); then the event the copy stream waits for
 // before it refills the window's buffer.
-int launch_window_digest(dsx_ctx* c, const DigestArgs& da, uint64_t max_n, int algo, int slot) {
+int launch_window_digest(dsx_ctx* c, const DigestArgs& da, uint64_t max_n, int algo, int slot,
+                         uint32_t max_blocks = 0) {
   HIPCHK(c, hipEventRecord(c->idx_stitch_ev[slot], c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->idx_dg_stream, c->idx_stitch_ev[slot], 0));
-  const int rc = launch_digest(c, da, max_n, algo, c->idx_dg_stream, nullptr, true);
+  const int rc = launch_digest(c, da, max_n, algo, c->idx_dg_stream, nullptr, true, max_blocks);
   if (rc) return rc;
   HIPCHK(c, hipEventRecord(c->idx_win_ev[slot], c->idx_dg_stream));
   return DSX_OK;
@@ -217,9 +218,7 @@ struct ProgressScope {
 // runs at the clock an idle-ish GPU has then, ~58 ns per byte, against ~38 ns
 // on a busy one; 16 host threads read and hash ~43 GB/s)
 constexpr double kGpuNsPerByte = 58.0;   // digest_pc_kernel, one lane, end of a file call
-#if DSX_DIAG
 constexpr double kReadBytesPerNs = 45.0;  // page cache -> HBM through the pinned slots (dsx_cut_fd, ~42 GiB/s)
-#endif
 constexpr double kHostNsPerByte = 0.38;  // one host thread, read + hash (AVX-512)
 constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
 constexpr int kTailThreads = 16;
@@ -354,11 +353,20 @@ class TailFeeder {
  public:
   // (the last of several windows: start_ev marks the previous window's
   // snapshot dsnap = {cuts before this window, their last end})
+  // (cut1: the cut of the chunks before the window's mid snapshot, set_mid;
+  // the GPU hashed the shorter ones during the read)
   TailFeeder(dsx_ctx* c, const TailSrc& src, uint64_t len, uint64_t cut, int threads,
-             uint64_t seq0, hipEvent_t start_ev = nullptr, const uint64_t* dsnap = nullptr)
-      : c_(c), src_(src), len_(len), cut_(cut), threads_(threads), seq0_(seq0),
+             uint64_t seq0, hipEvent_t start_ev, const uint64_t* dsnap, uint64_t cut1)
+      : c_(c), src_(src), len_(len), cut_(cut), cut1_(cut1), threads_(threads), seq0_(seq0),
         start_ev_(start_ev), dsnap_(dsnap) {
     th_ = std::thread([this] { run(); });
+  }
+  // the mid snapshot {total, carry} was enqueued (mid_ev after it): chunks
+  // from its total on take the usual cut
+  void set_mid(hipEvent_t mid_ev, const uint64_t* mid_snap) {
+    std::lock_guard<std::mutex> g(m_);
+    mid_ev_ = mid_ev;
+    mid_snap_ = mid_snap;
   }
   ~TailFeeder() { stop(); }
   void finish(uint64_t total) {
@@ -419,15 +427,34 @@ class TailFeeder {
       seen = sn[0];
       prev = sn[1];
     }
+    uint64_t mid_total = UINT64_MAX;  // chunks [0, mid_total) take cut1_ (until set_mid: all)
+    bool mid_known = false;
     while (true) {
       uint64_t target;
       bool last;
+      hipEvent_t mev = nullptr;
+      const uint64_t* msnap = nullptr;
       {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait_for(g, std::chrono::microseconds(200), [&] { return stop_ || have_final_; });
         if (stop_) break;
         last = have_final_;
+        // (read with the mid flag under one lock: a total published before
+        // set_mid cannot come from a piece after the mid snapshot)
         target = last ? final_ : std::max(seen, published());
+        mev = mid_ev_;
+        msnap = mid_snap_;
+      }
+      if (mev && !mid_known) {
+        uint64_t sn[2] = {0, 0};
+        if (hipEventSynchronize(mev) != hipSuccess ||
+            hipMemcpyAsync(sn, msnap, sizeof sn, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+          err_ = DSX_E_HIP;
+          break;
+        }
+        mid_total = sn[0];
+        mid_known = true;
       }
       if (target > seen) {
         e.resize(target - seen);
@@ -442,7 +469,8 @@ class TailFeeder {
           const uint64_t st = i ? e[i - 1] : prev;
           // (a call that overflows its candidate slots reruns and drops these:
           // never read outside the source for them)
-          if (e[i] > st && e[i] <= len_ && e[i] - st > cut_) batch.push_back({seen + i, st, e[i] - st});
+          const uint64_t cut = seen + i < mid_total ? cut1_ : cut_;
+          if (e[i] > st && e[i] <= len_ && e[i] - st > cut) batch.push_back({seen + i, st, e[i] - st});
         }
         prev = e.back();
         seen = target;
@@ -466,7 +494,9 @@ class TailFeeder {
   dsx_ctx* c_;
   TailSrc src_;
   uint64_t len_;
-  uint64_t cut_;
+  uint64_t cut_, cut1_;
+  hipEvent_t mid_ev_ = nullptr;  // (set_mid, under m_)
+  const uint64_t* mid_snap_ = nullptr;
   int threads_;
   uint64_t seq0_;
   hipEvent_t start_ev_;
@@ -594,28 +624,33 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     std::unique_ptr<TailFeeder> feed;
     const int fth = feed_threads(c);
     const uint64_t fcut = feed_cut(c, fth);
-    // (Diagnostic) one window (a file up to DSX_INDEX_WINDOW): its first `mid` bytes are
-    // hashed on the GPU WHILE the rest is read -- a digest on the digest
-    // stream over the chunks stitched by then, every size (its chain, at most
-    // max bytes, ends before the read does) -- and the tail feeder starts at
-    // that point, so the host hashes only the long chunks after it.  mid is
-    // where the remaining read time covers the longest chain: (1 - mid/len)
-    // x the read time >= max x kGpuNsPerByte, at most half the window.  (The
-    // host, at the process's CPU share, cannot keep up with the long chunks
-    // of a whole window)
-    uint64_t mid_at = 0;
+    // One window (a file up to DSX_INDEX_WINDOW), two cuts.  The GPU hashes
+    // the window's first part DURING the read: a digest on the digest stream
+    // once the piece at `mid_at` is stitched, over the chunks confirmed by
+    // then, all but those longer than cut1 -- its chain (cut1 x 58 ns) ends
+    // before the read does.  The feeder hashes, from the call's start, the
+    // first part's chunks above cut1 and the rest's above the usual cut; the
+    // digest after the read takes the rest's short chunks.  The host then has
+    // ~40 % fewer bytes than with one cut over the whole window (DESIGN.md
+    // 5.1).  mid_at: half the window; cut1 = the read time left after it over
+    // the GPU's ns per byte; off when that is not twice the usual cut (files
+    // below ~0.6 GiB), for SHA-256, or without the host tail.
+    // (A first form gave the GPU every chunk of the first part and started
+    // the feeder at mid: the host then had less time for the same work, 0.66-
+    // 0.72 x dsx_cut_fd against 0.78, profiles/r06e, r06f.)
+    uint64_t mid_at = 0, cut1 = 0;
+    if (tail_on && nwin == 1 && c->index_host_tail < 0) {
+      double frac = 0.5;
 #if DSX_DIAG
-    // (measured, not kept: the host, which then starts at mid, finished
-    // later -- 0.72 x dsx_cut_fd against 0.78 without, profiles/r06e; the
-    // diagnostic build keeps it behind DSX_FEED_MID for the record)
-    if (tail_on && nwin == 1 && getenv("DSX_FEED_MID")) {
-      const double t_read = (double)len / kReadBytesPerNs;     // ns
-      double frac = 1.0 - (double)p->max * kGpuNsPerByte / t_read;
-      frac = std::min(frac, 0.5);
-      frac = std::min(frac, atof(getenv("DSX_FEED_MID")));
-      if (frac >= 0.1) mid_at = (uint64_t)(frac * (double)len);
-    }
+      if (const char* v = getenv("DSX_FEED_MID")) frac = atof(v);  // (0: off; A/B)
 #endif
+      const double t_read = (double)len / kReadBytesPerNs;  // ns
+      const double c1 = (1.0 - frac) * t_read / kGpuNsPerByte;
+      if (frac > 0.05 && frac < 0.95 && c1 >= 2.0 * (double)fcut) {
+        mid_at = (uint64_t)(frac * (double)len);
+        cut1 = std::min<uint64_t>(p->max, (uint64_t)c1 & ~4095ull);
+      }
+    }
     uint64_t* const mid_snap = c->idx_snap.p + 2 * (nwin + 1);
     bool mid_done = false;
     for (w = 0; w < nwin; ++w) {
@@ -626,9 +661,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #if DSX_DIAG
       if (nwin > 1 && getenv("DSX_FEED_MULTI") && atoi(getenv("DSX_FEED_MULTI")) == 0) feed_on = false;
 #endif
-      if (feed_on && !mid_at) {
+      if (feed_on) {
         feed.reset(new TailFeeder(c, tsrc, len, fcut, fth, c->piece_seq,
-                                  nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w));
+                                  nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w,
+                                  mid_at ? cut1 : fcut));
       }
       // the digest of window w-2 read this buffer; the copy stream waits for it
       if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
@@ -661,8 +697,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           c->timing = true;
           if (rc) return drain(c, pf, rc);
           scanned = end;
-          if (mid_at && !mid_done && end >= mid_at && end < len) {
+          if (mid_at && !mid_done && end >= mid_at && end < len && feed) {
             // the GPU's share of the one window: chunks [0, mid_snap.total)
+            // up to cut1, on the digest stream, on 3/4 of the CUs (the rest
+            // keep room for the next pieces' scans)
             mid_done = true;
             hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
                                (const DevState*)c->state.p, mid_snap);
@@ -676,13 +714,15 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
             dm.ids = c->dg_ids.p;
             dm.range_lo = c->idx_snap.p;
             dm.range_hi = mid_snap;
-            rc = launch_window_digest(c, dm, end / p->min + 2, algo, 0);
+            dm.skip_above = cut1 >= p->max ? 0 : cut1;
+            rc = launch_window_digest(c, dm, end / p->min + 2, algo, 0, (uint32_t)(c->ncu * 3 / 4));
             if (rc) return drain(c, pf, rc);
-            feed.reset(new TailFeeder(c, tsrc, len, fcut, fth, c->piece_seq, feed_ev.e, mid_snap));
+            feed->set_mid(feed_ev.e, mid_snap);
 #if DSX_DIAG
             if (getenv("DSX_TAIL_LOG"))
-              fprintf(stderr, "index: GPU share of the window up to %.1f MB, %.2f ms into the call\n",
-                      end / 1e6, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
+              fprintf(stderr, "index: GPU share of the window up to %.1f MB (cut1 %lu), %.2f ms into the call\n",
+                      end / 1e6, (unsigned long)cut1,
+                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
 #endif
           }
 #if DSX_DIAG

@@ -136,6 +136,52 @@ def test_index_host_threads(tmp_path, monkeypatch, threads):
             assert n_host == int(np.sum(lens > 131072))
 
 
+def test_index_host_tail_two_cuts(tmp_path, monkeypatch):
+    """One window large enough for the GPU's share during the read (the
+    digest of the first half's chunks up to cut1 on the digest stream, the
+    feeder taking the first half's chunks above cut1 and the rest's above the
+    usual cut): every ID is hashlib's, and the host took between the chunks
+    above cut1 and those above the usual cut.  32 host threads -> 28
+    feeders, cut 28 KiB; 320 MiB -> cut1 = 0.5 x 320 MiB / 45 B/ns / 58 ns
+    rounded down to 4 KiB = 61440."""
+    import concurrent.futures as cf
+
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_HOST_THREADS", "32")
+    n = (320 << 20) + 4321
+    data = o.synth_uniform_c(48, 0, n)
+    f = tmp_path / "blob"
+    data.tofile(str(f))
+    ctx = _lib.Context(0)
+    try:
+        fd = os.open(str(f), os.O_RDONLY)
+        try:
+            ends, ids = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+        finally:
+            os.close(fd)
+        n_host = ctx.stats().host_tail_chunks
+        ends2, ids2 = desync_amd.index_host(data, MIN, AVG, MAX, ctx=ctx)
+    finally:
+        ctx.close()
+    ref = o.chunk_parallel(data, MIN, AVG, MAX, o.default_threads())
+    assert np.array_equal(ends, ref) and np.array_equal(ends2, ref)
+    starts = np.concatenate([[0], ref[:-1]]).astype(np.uint64)
+    mv = memoryview(data)
+
+    def h(i):
+        return hashlib.new("sha512_256", mv[int(starts[i]):int(ref[i])]).digest()
+
+    with cf.ThreadPoolExecutor(o.default_threads()) as pool:
+        want = list(pool.map(h, range(ref.size), chunksize=256))
+    assert [bytes(x) for x in ids] == want
+    assert [bytes(x) for x in ids2] == want
+    avx512 = "avx512f" in open("/proc/cpuinfo").read() and "avx512bw" in open("/proc/cpuinfo").read()
+    if avx512:
+        lens = (ref - starts).astype(np.int64)
+        assert int(np.sum(lens > 61440)) <= n_host < int(np.sum(lens > 28672)), n_host
+
+
 @pytest.mark.parametrize("tail,window", [("65536", 16 << 20), ("0", 16 << 20), ("-1", 16 << 20),
                                          ("100000", None), ("-1", None)])
 def test_index_host_tail(tmp_path, monkeypatch, tail, window):

@@ -86,10 +86,13 @@ def main():
                         os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
                         # (a name ending in `_nomulti`: no feeder on the last of several windows)
                         os.environ["DSX_FEED_MULTI"] = "0" if name.endswith("_nomulti") else "1"
-                        # (a name ending in `_mid`: the GPU's share of a one-window
-                        # file, DSX_FEED_MID=0.5 in the diagnostic build)
-                        if name.endswith("_mid"):
-                            os.environ["DSX_FEED_MID"] = "0.5"
+                        # (a name ending in `_nomid`: no GPU share of a one-window file
+                        # during the read, DSX_FEED_MID=0 in the diagnostic build;
+                        # `_midF`: the share up to the fraction 0.F of the file)
+                        if name.endswith("_nomid"):
+                            os.environ["DSX_FEED_MID"] = "0"
+                        elif "_mid" in name:
+                            os.environ["DSX_FEED_MID"] = "0." + name.split("_mid")[1]
                         else:
                             os.environ.pop("DSX_FEED_MID", None)
                         t0 = time.perf_counter()
