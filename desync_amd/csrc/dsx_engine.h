@@ -315,6 +315,13 @@ struct dsx_ctx {
   // chain, ~10-15 ms) does not hold the next window's scans and stitches on
   // `stream` (nor the tail feeder, which follows their published totals)
   hipStream_t idx_dg_stream = nullptr;
+  // the GPU's shares of a one-window call during its read (dsx_index.cpp), one
+  // stream each so that they run side by side, each with its queue counter
+  // (idx_side_q[32 k], one 128-B line each); low priority like idx_dg_stream:
+  // the runtime's low-priority pool then holds exactly these four
+  static constexpr int kIdxSide = 3;
+  hipStream_t idx_side[kIdxSide] = {};
+  DevBuf<uint32_t> idx_side_q;
   hipEvent_t q_ev[kQueueDepth] = {};
   uint32_t q_next = 0;
 };
@@ -372,6 +379,11 @@ void host_parallel(int parts, const std::function<void(int)>& fn);
 // cgroup v2 quota and OMP_NUM_THREADS (the GPU box's per-GPU share), or
 // DSX_HOST_THREADS when set
 int host_cpu_share();
+// a stream for work beside the pipeline (window digests, the tail feeder's
+// copies; dsx_stream.cpp): the lowest priority, so it takes an HSA queue of
+// the runtime's low-priority pool instead of sharing one with the scan or
+// copy stream (GPU_MAX_HW_QUEUES per pool, 4 on the box, tools/queue_probe)
+hipError_t side_stream_create(hipStream_t* s);
 // SHA-512/256 on the host (dsx_hostsha.cpp): one message, or 8 at once in
 // AVX-512 lanes (only when host_sha_vec(); n[i] == UINT64_MAX: unused lane)
 bool host_sha_vec();

@@ -165,7 +165,10 @@ int index_setup(dsx_ctx* c, uint64_t slot_bytes) {
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : c->idx_stitch_ev)
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (!c->idx_dg_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->idx_dg_stream, hipStreamNonBlocking));
+  if (!c->idx_dg_stream) HIPCHK(c, side_stream_create(&c->idx_dg_stream));
+  for (auto& s : c->idx_side)
+    if (!s) HIPCHK(c, side_stream_create(&s));
+  HIPCHK(c, c->idx_side_q.ensure(32 * dsx_ctx::kIdxSide));
   return DSX_OK;
 }
 
@@ -190,6 +193,8 @@ int drain(dsx_ctx* c, Prefetcher& pf, int rc) {
   (void)hipStreamSynchronize(c->scan_stream);
   (void)hipStreamSynchronize(c->stream);
   if (c->idx_dg_stream) (void)hipStreamSynchronize(c->idx_dg_stream);
+  for (auto& s : c->idx_side)
+    if (s) (void)hipStreamSynchronize(s);
   return rc;
 }
 
@@ -222,6 +227,7 @@ constexpr double kReadBytesPerNs = 45.0;  // page cache -> HBM through the pinne
 constexpr double kHostNsPerByte = 0.38;  // one host thread, read + hash (AVX-512)
 constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
 constexpr int kTailThreads = 16;
+constexpr size_t kMaxMids = dsx_ctx::kIdxSide;  // GPU shares of a one-window call during its read
 
 struct TailChunk {
   uint64_t idx, start, len;
@@ -353,20 +359,22 @@ class TailFeeder {
  public:
   // (the last of several windows: start_ev marks the previous window's
   // snapshot dsnap = {cuts before this window, their last end})
-  // (cut1: the cut of the chunks before the window's mid snapshot, set_mid;
-  // the GPU hashed the shorter ones during the read)
+  // (`cut`: the cut of the chunks before the first boundary; a boundary, a
+  // snapshot the GPU hashed the shorter chunks before during the read, sets
+  // the cut of those after it)
   TailFeeder(dsx_ctx* c, const TailSrc& src, uint64_t len, uint64_t cut, int threads,
-             uint64_t seq0, hipEvent_t start_ev, const uint64_t* dsnap, uint64_t cut1)
-      : c_(c), src_(src), len_(len), cut_(cut), cut1_(cut1), threads_(threads), seq0_(seq0),
+             uint64_t seq0, hipEvent_t start_ev = nullptr, const uint64_t* dsnap = nullptr)
+      : c_(c), src_(src), len_(len), cut_(cut), threads_(threads), seq0_(seq0),
         start_ev_(start_ev), dsnap_(dsnap) {
     th_ = std::thread([this] { run(); });
   }
-  // the mid snapshot {total, carry} was enqueued (mid_ev after it): chunks
-  // from its total on take the usual cut
-  void set_mid(hipEvent_t mid_ev, const uint64_t* mid_snap) {
+  // a snapshot {total, carry} was enqueued (ev after it): chunks from its
+  // total on take `cut_after`.  Called before the pieces after the snapshot
+  // are enqueued, so no total the feeder reads after it can come from them
+  // without it knowing the boundary.
+  void add_boundary(hipEvent_t ev, const uint64_t* snap, uint64_t cut_after) {
     std::lock_guard<std::mutex> g(m_);
-    mid_ev_ = mid_ev;
-    mid_snap_ = mid_snap;
+    bounds_.push_back({ev, snap, cut_after, 0});
   }
   ~TailFeeder() { stop(); }
   void finish(uint64_t total) {
@@ -408,6 +416,8 @@ class TailFeeder {
       err_ = DSX_E_HIP;
       return;
     }
+    // (normal priority: with the null stream, `stream` and `copy_stream` the
+    // fourth queue of that pool; the low-priority pool is the digests')
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
       err_ = DSX_E_HIP;
@@ -427,35 +437,33 @@ class TailFeeder {
       seen = sn[0];
       prev = sn[1];
     }
-    uint64_t mid_total = UINT64_MAX;  // chunks [0, mid_total) take cut1_ (until set_mid: all)
-    bool mid_known = false;
+    std::vector<Bound> known;  // the boundaries resolved so far (their totals read)
     while (true) {
       uint64_t target;
       bool last;
-      hipEvent_t mev = nullptr;
-      const uint64_t* msnap = nullptr;
+      std::vector<Bound> fresh;
       {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait_for(g, std::chrono::microseconds(200), [&] { return stop_ || have_final_; });
         if (stop_) break;
         last = have_final_;
-        // (read with the mid flag under one lock: a total published before
-        // set_mid cannot come from a piece after the mid snapshot)
+        // (read with the boundaries under one lock: a total published before
+        // add_boundary cannot come from a piece after that snapshot)
         target = last ? final_ : std::max(seen, published());
-        mev = mid_ev_;
-        msnap = mid_snap_;
+        fresh.assign(bounds_.begin() + (long)known.size(), bounds_.end());
       }
-      if (mev && !mid_known) {
+      for (Bound& b : fresh) {
         uint64_t sn[2] = {0, 0};
-        if (hipEventSynchronize(mev) != hipSuccess ||
-            hipMemcpyAsync(sn, msnap, sizeof sn, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        if (hipEventSynchronize(b.ev) != hipSuccess ||
+            hipMemcpyAsync(sn, b.snap, sizeof sn, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
           err_ = DSX_E_HIP;
           break;
         }
-        mid_total = sn[0];
-        mid_known = true;
+        b.total = sn[0];
+        known.push_back(b);
       }
+      if (err_) break;
       if (target > seen) {
         e.resize(target - seen);
         if (hipMemcpyAsync(e.data(), c_->out.p + seen, e.size() * 8, hipMemcpyDeviceToHost, s) !=
@@ -469,7 +477,9 @@ class TailFeeder {
           const uint64_t st = i ? e[i - 1] : prev;
           // (a call that overflows its candidate slots reruns and drops these:
           // never read outside the source for them)
-          const uint64_t cut = seen + i < mid_total ? cut1_ : cut_;
+          uint64_t cut = cut_;
+          for (const Bound& b : known)
+            if (seen + i >= b.total) cut = b.cut_after;
           if (e[i] > st && e[i] <= len_ && e[i] - st > cut) batch.push_back({seen + i, st, e[i] - st});
         }
         prev = e.back();
@@ -494,9 +504,13 @@ class TailFeeder {
   dsx_ctx* c_;
   TailSrc src_;
   uint64_t len_;
-  uint64_t cut_, cut1_;
-  hipEvent_t mid_ev_ = nullptr;  // (set_mid, under m_)
-  const uint64_t* mid_snap_ = nullptr;
+  uint64_t cut_;
+  struct Bound {
+    hipEvent_t ev;
+    const uint64_t* snap;
+    uint64_t cut_after, total;
+  };
+  std::vector<Bound> bounds_;  // (add_boundary, under m_)
   int threads_;
   uint64_t seq0_;
   hipEvent_t start_ev_;
@@ -556,7 +570,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   if (rc) return rc;
   HIPCHK(c, grow(c, c->idx_win[0], pre + W));
   if (nwin > 1) HIPCHK(c, grow(c, c->idx_win[1], pre + W));
-  HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 2)));  // (+1: the one window's mid snapshot)
+  HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 1 + kMaxMids)));  // (+ the one window's mid snapshots)
   HIPCHK(c, grow(c, c->out, need));
   if (algo >= 0) HIPCHK(c, grow(c, c->dg_ids, need * 32));
   const int K = dsx_ctx::kIdxSlots;
@@ -624,35 +638,58 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     std::unique_ptr<TailFeeder> feed;
     const int fth = feed_threads(c);
     const uint64_t fcut = feed_cut(c, fth);
-    // One window (a file up to DSX_INDEX_WINDOW), two cuts.  The GPU hashes
-    // the window's first part DURING the read: a digest on the digest stream
-    // once the piece at `mid_at` is stitched, over the chunks confirmed by
-    // then, all but those longer than cut1 -- its chain (cut1 x 58 ns) ends
-    // before the read does.  The feeder hashes, from the call's start, the
-    // first part's chunks above cut1 and the rest's above the usual cut; the
-    // digest after the read takes the rest's short chunks.  The host then has
-    // ~40 % fewer bytes than with one cut over the whole window (DESIGN.md
-    // 5.1).  mid_at: half the window; cut1 = the read time left after it over
-    // the GPU's ns per byte; off when that is not twice the usual cut (files
-    // below ~0.6 GiB), for SHA-256, or without the host tail.
-    // (A first form gave the GPU every chunk of the first part and started
+    // One window (a file up to DSX_INDEX_WINDOW): the GPU hashes most of it
+    // DURING the read.  At the points f_k of the window (1/2, 3/4, 7/8, ...)
+    // a snapshot follows the piece's stitch and a digest on the digest stream
+    // hashes the chunks confirmed since the previous point, all but those
+    // longer than cut_k = the read time left after f_k over the GPU's ns per
+    // byte: its chain ends about when the read does.  The feeder hashes, from
+    // the call's start, each segment's chunks above its cut and the last
+    // segment's above `fcut`; the digest after the read takes the last
+    // segment's short chunks, a chain of at most fcut bytes.  The points stop
+    // where cut_k would fall below 1.5 x fcut; none when the first is below
+    // 2 x fcut (files below ~0.6 GiB), for SHA-256, or without the host tail.
+    // The digest stream has a hardware queue of its own (side_stream_create):
+    // on one shared with the pipeline's streams these digests held the next
+    // pieces' scans and the call fell to 0.58-0.63 x dsx_cut_fd
+    // (profiles/r06q, r06x).
+    // (A first form gave the GPU every chunk of the first half and started
     // the feeder at mid: the host then had less time for the same work, 0.66-
     // 0.72 x dsx_cut_fd against 0.78, profiles/r06e, r06f.)
-    uint64_t mid_at = 0, cut1 = 0;
+    struct Mid {
+      uint64_t at, cut;
+    };
+    std::vector<Mid> mids;
+    uint64_t fcut_end = fcut;
     if (tail_on && nwin == 1 && c->index_host_tail < 0) {
-      double frac = 0.5;
-#if DSX_DIAG
-      if (const char* v = getenv("DSX_FEED_MID")) frac = atof(v);  // (0: off; A/B)
-#endif
       const double t_read = (double)len / kReadBytesPerNs;  // ns
-      const double c1 = (1.0 - frac) * t_read / kGpuNsPerByte;
-      if (frac > 0.05 && frac < 0.95 && c1 >= 2.0 * (double)fcut) {
-        mid_at = (uint64_t)(frac * (double)len);
-        cut1 = std::min<uint64_t>(p->max, (uint64_t)c1 & ~4095ull);
+      std::vector<double> fr;
+      for (double f = 0.5; f < 0.99 && fr.size() < kMaxMids; f = 0.5 * (1.0 + f)) fr.push_back(f);
+#if DSX_DIAG
+      if (const char* v = getenv("DSX_FEED_MID")) {  // (A/B: "0" off, else a list "0.5,0.75")
+        fr.clear();
+        for (const char* q = v; *q && fr.size() < kMaxMids;) {
+          char* nx = nullptr;
+          const double f = strtod(q, &nx);
+          if (nx == q) break;
+          if (f > 0.05 && f < 0.99 && (fr.empty() || f > fr.back())) fr.push_back(f);
+          q = *nx == ',' ? nx + 1 : nx;
+        }
       }
+      if (const char* v = getenv("DSX_FEED_CUT_END")) fcut_end = std::max<uint64_t>(4096, atol(v));
+#endif
+      for (double f : fr) {
+        const double ck = (1.0 - f) * t_read / kGpuNsPerByte;
+        if (ck < (mids.empty() ? 2.0 : 1.5) * (double)fcut_end) break;
+        mids.push_back({(uint64_t)(f * (double)len), std::min<uint64_t>(p->max, (uint64_t)ck & ~4095ull)});
+      }
+      if (mids.empty()) fcut_end = fcut;
     }
-    uint64_t* const mid_snap = c->idx_snap.p + 2 * (nwin + 1);
-    bool mid_done = false;
+    std::vector<Ev> mid_ev(mids.size());
+    for (auto& x : mid_ev) HIPCHK(c, hipEventCreateWithFlags(&x.e, hipEventDisableTiming));
+    size_t mids_done = 0;
+    // snapshot k: after the piece at mids[k].at (the window's start is idx_snap[0])
+    auto mid_snap = [&](size_t k) { return c->idx_snap.p + 2 * (nwin + 1 + k); };
     for (w = 0; w < nwin; ++w) {
       ws = w * W;
       wl = std::min(W, len - ws);
@@ -662,9 +699,8 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       if (nwin > 1 && getenv("DSX_FEED_MULTI") && atoi(getenv("DSX_FEED_MULTI")) == 0) feed_on = false;
 #endif
       if (feed_on) {
-        feed.reset(new TailFeeder(c, tsrc, len, fcut, fth, c->piece_seq,
-                                  nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w,
-                                  mid_at ? cut1 : fcut));
+        feed.reset(new TailFeeder(c, tsrc, len, mids.empty() ? fcut : mids[0].cut, fth,
+                                  c->piece_seq, nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w));
       }
       // the digest of window w-2 read this buffer; the copy stream waits for it
       if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
@@ -697,14 +733,14 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           c->timing = true;
           if (rc) return drain(c, pf, rc);
           scanned = end;
-          if (mid_at && !mid_done && end >= mid_at && end < len && feed) {
-            // the GPU's share of the one window: chunks [0, mid_snap.total)
-            // up to cut1, on the digest stream, on 3/4 of the CUs (the rest
-            // keep room for the next pieces' scans)
-            mid_done = true;
+          if (mids_done < mids.size() && end >= mids[mids_done].at && end < len && feed) {
+            // the GPU's share of segment k: chunks [snap[k-1].total,
+            // snap[k].total) up to its cut, on the digest stream, on 3/4 of
+            // the CUs (the rest keep room for the next pieces' scans)
+            const size_t m = mids_done++;
             hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
-                               (const DevState*)c->state.p, mid_snap);
-            e = hipEventRecord(feed_ev.e, c->stream);
+                               (const DevState*)c->state.p, mid_snap(m));
+            e = hipEventRecord(mid_ev[m].e, c->stream);
             if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
             DigestArgs dm{};
             dm.blob = buf + pre;
@@ -712,16 +748,21 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
             dm.len = end;
             dm.ends = c->out.p;
             dm.ids = c->dg_ids.p;
-            dm.range_lo = c->idx_snap.p;
-            dm.range_hi = mid_snap;
-            dm.skip_above = cut1 >= p->max ? 0 : cut1;
-            rc = launch_window_digest(c, dm, end / p->min + 2, algo, 0, (uint32_t)(c->ncu * 3 / 4));
+            dm.range_lo = m ? mid_snap(m - 1) : c->idx_snap.p;
+            dm.range_hi = mid_snap(m);
+            dm.skip_above = mids[m].cut >= p->max ? 0 : mids[m].cut;
+            // (on side stream m after this stitch: the shares run side by side)
+            hipStream_t ss = c->idx_side[m];
+            e = hipStreamWaitEvent(ss, mid_ev[m].e, 0);
+            if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: wait"));
+            rc = launch_digest(c, dm, end / p->min + 2, algo, ss, c->idx_side_q.p + 32 * m, false,
+                               (uint32_t)(c->ncu * 3 / 4));
             if (rc) return drain(c, pf, rc);
-            feed->set_mid(feed_ev.e, mid_snap);
+            feed->add_boundary(mid_ev[m].e, mid_snap(m), m + 1 < mids.size() ? mids[m + 1].cut : fcut_end);
 #if DSX_DIAG
             if (getenv("DSX_TAIL_LOG"))
-              fprintf(stderr, "index: GPU share of the window up to %.1f MB (cut1 %lu), %.2f ms into the call\n",
-                      end / 1e6, (unsigned long)cut1,
+              fprintf(stderr, "index: GPU share %zu up to %.1f MB (cut %lu), %.2f ms into the call\n",
+                      m, end / 1e6, (unsigned long)mids[m].cut,
                       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
 #endif
           }
@@ -751,7 +792,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       da.len = w == 0 ? wl : pre + wl;
       da.ends = c->out.p;
       da.ids = c->dg_ids.p;
-      da.range_lo = mid_done ? mid_snap : c->idx_snap.p + 2 * w;  // (after the GPU's share)
+      da.range_lo = mids_done ? mid_snap(mids_done - 1) : c->idx_snap.p + 2 * w;  // (after the GPU's shares)
       da.range_hi = c->idx_snap.p + 2 * (w + 1);
       if (tail_on && w + 1 == nwin) {
         // the window's chunk ends (the stitch is done once the stream is)
@@ -767,7 +808,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: tail ends"));
         const int threads = std::max(1, std::min(kTailThreads, host_cpu_share()));
         if (feed) {  // the feeder has the long chunks: the GPU the rest
-          da.skip_above = fcut;
+          da.skip_above = fcut_end;
           rc = launch_window_digest(c, da, (pre + wl) / p->min + 2, algo, (int)(w & 1));
           if (rc) return drain(c, pf, rc);
 #if DSX_DIAG
@@ -830,6 +871,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     rc = read_state(c, &st);  // (the stitches)
     HIPCHK(c, hipStreamSynchronize(c->copy_stream));
     HIPCHK(c, hipStreamSynchronize(c->idx_dg_stream));  // (the digests)
+    for (size_t m = 0; m < mids_done; ++m) HIPCHK(c, hipStreamSynchronize(c->idx_side[m]));
     if (rc) return rc;
     if (st.err & kErrDense) {  // rare: a lane overflowed its candidate slots
       c->stats.dense_fallbacks++;
@@ -1055,6 +1097,9 @@ void index_release(dsx_ctx* c) {
     (void)hipStreamDestroy(c->idx_dg_stream);
     c->idx_dg_stream = nullptr;
   }
+  for (auto& s : c->idx_side)
+    if (s) (void)hipStreamSynchronize(s), (void)hipStreamDestroy(s), s = nullptr;
+  c->idx_side_q.release();
   for (auto& e : c->idx_stitch_ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   for (auto& s : c->idx_slots) {

@@ -86,15 +86,24 @@ def main():
                         os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
                         # (a name ending in `_nomulti`: no feeder on the last of several windows)
                         os.environ["DSX_FEED_MULTI"] = "0" if name.endswith("_nomulti") else "1"
-                        # (a name ending in `_nomid`: no GPU share of a one-window file
+                        # (`_nomid` in the name: no GPU share of a one-window file
                         # during the read, DSX_FEED_MID=0 in the diagnostic build;
-                        # `_midF`: the share up to the fraction 0.F of the file)
-                        if name.endswith("_nomid"):
-                            os.environ["DSX_FEED_MID"] = "0"
-                        elif "_mid" in name:
-                            os.environ["DSX_FEED_MID"] = "0." + name.split("_mid")[1]
-                        else:
-                            os.environ.pop("DSX_FEED_MID", None)
+                        # `_mK`: the shares at the first K points 1/2, 3/4, 7/8, ...;
+                        # `_eN`: the last segment's cut N KiB, DSX_FEED_CUT_END)
+                        parts = name.split("_")[1:]
+                        os.environ.pop("DSX_FEED_MID", None)
+                        os.environ.pop("DSX_FEED_CUT_END", None)
+                        for part in parts:
+                            if part == "nomid":
+                                os.environ["DSX_FEED_MID"] = "0"
+                            elif part[:1] == "m" and part[1:].isdigit():
+                                pts, f = [], 0.5
+                                for _ in range(int(part[1:])):
+                                    pts.append(repr(f))
+                                    f = 0.5 * (1 + f)
+                                os.environ["DSX_FEED_MID"] = ",".join(pts) or "0"
+                            elif part[:1] == "e" and part[1:].isdigit():
+                                os.environ["DSX_FEED_CUT_END"] = str(int(part[1:]) << 10)
                         t0 = time.perf_counter()
                         desync_amd.index_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
                     times[name] = time.perf_counter() - t0
