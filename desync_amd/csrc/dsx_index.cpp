@@ -728,20 +728,25 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     const int fth = feed_threads(c);
     const uint64_t fcut = feed_cut(c, fth);
     // One window (a file up to DSX_INDEX_WINDOW): the GPU hashes most of it
-    // DURING the read.  At the points f_k of the window (1/2, 3/4, 7/8, ...)
-    // a snapshot follows the piece's stitch and a digest on the digest stream
-    // hashes the chunks confirmed since the previous point, all but those
-    // longer than cut_k = the read time left after f_k over the GPU's ns per
-    // byte: its chain ends about when the read does.  The feeder hashes, from
-    // the call's start, each segment's chunks above its cut and the last
-    // segment's above `fcut`; the digest after the read takes the last
-    // segment's short chunks, a chain of at most fcut bytes.  The points stop
-    // where cut_k would fall below 1.5 x fcut; none when the first is below
-    // 2 x fcut (files below ~0.6 GiB), for SHA-256, or without the host tail.
-    // The digest stream has a hardware queue of its own (side_stream_create):
-    // on one shared with the pipeline's streams these digests held the next
+    // DURING the read.  At the points f_k of the window (1/2, 3/4, ...) a
+    // snapshot follows the piece's stitch and a digest on side stream k (a
+    // "share") hashes the chunks confirmed since the previous point, all but
+    // those longer than cut_k = the read time left after f_k over the GPU's
+    // ns per byte: its chain ends about when the read does.  The feeder
+    // hashes, from the call's start, each segment's chunks above its cut and
+    // the last segment's above fcut_end; the digest after the read (on
+    // `stream`, digest_pc_kernel) takes the last segment's short chunks, a
+    // chain of at most fcut_end bytes.  The points stop where cut_k would
+    // fall below 1.25 x fcut_end (two points at 1 GiB and 12 threads); none
+    // when the first is below 2 x fcut_end (files below ~0.6 GiB), for
+    // SHA-256, or without the host tail.  At 1 GiB and 12 threads the host
+    // takes 2,985 chunks against 6,060 without the shares, and the call
+    // reads 0.87-0.90 x dsx_cut_fd against 0.78-0.84.
+    // The side streams have hardware queues of their own (side_stream_create):
+    // on one shared with the pipeline's streams the shares held the next
     // pieces' scans and the call fell to 0.58-0.63 x dsx_cut_fd
-    // (profiles/r06q, r06x).
+    // (profiles/r06q, r06x).  Four shares (down to 7/8 and 15/16) slowed the
+    // read: 0.87 against 0.89 (profiles/r06ag).
     // (A first form gave the GPU every chunk of the first half and started
     // the feeder at mid: the host then had less time for the same work, 0.66-
     // 0.72 x dsx_cut_fd against 0.78, profiles/r06e, r06f.)
@@ -759,6 +764,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     if (const char* v = getenv("DSX_SHARE_PC")) share_pc = atoi(v);
 #endif
     if (tail_on && nwin == 1 && c->index_host_tail < 0) {
+      // with the shares the host has fewer bytes: 3/4 of the usual cut
+      // after the last point (64 -> 48 KiB at 12 threads; profiles/r06af,
+      // r06ag: 0.882 / 0.898 x dsx_cut_fd against 0.874 / 0.894)
+      fcut_end = std::max<uint64_t>(kFeedCutBase, (fcut * 3 / 4) & ~4095ull);
       const double t_read = (double)len / kReadBytesPerNs;  // ns
       std::vector<double> fr;
       for (double f = 0.5; f < 0.99 && fr.size() < kMaxMids; f = 0.5 * (1.0 + f)) fr.push_back(f);
