@@ -1358,7 +1358,7 @@ extern "C" int dsx_gen_dedup(dsx_ctx_t* c, void* d_dst, uint64_t offset, uint64_
 // (the grid is sized from it; with da.range_lo the count is read on the
 // device).
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream,
-                  uint32_t* queue, bool serial) {
+                  uint32_t* queue, bool serial, uint32_t max_blocks, int pc) {
   // the ctx stream, or a stream whose digests the caller runs one after
   // another (serial: dsx_index_*'s digest stream): the size-order scratch
   // (dg_order, dg_cls) is then never used by two launches at once
@@ -1371,8 +1371,10 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
   // split producer/consumer kernel: one workgroup (producer + consumer wave)
   // per CU, up to digest_pc_chunks chunks per lane of the grid
   const uint64_t pc_lanes = (uint64_t)c->ncu * 64u;
-  if (c->digest_pc > 0 || (c->digest_pc < 0 && max_n <= pc_lanes * (uint64_t)c->digest_pc_chunks)) {
-    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((max_n + 63) / 64, c->ncu));
+  if (c->digest_pc >= 0) pc = c->digest_pc > 0 ? 1 : 0;  // (DSX_DIGEST_PC)
+  if (pc > 0 || (pc < 0 && max_n <= pc_lanes * (uint64_t)c->digest_pc_chunks)) {
+    uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((max_n + 63) / 64, c->ncu));
+    if (max_blocks) blocks = std::min<uint64_t>(blocks, max_blocks);
     HIPCHK(c, hipMemsetAsync(queue, 0, 4, stream));
     da.queue = queue;
     da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * 64u);
@@ -1404,9 +1406,10 @@ int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream
 #endif
   HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kDigestThreads, 0));
   if (per_cu < 1) per_cu = 1;
-  const uint64_t blocks = std::max<uint64_t>(
+  uint64_t blocks = std::max<uint64_t>(
       1, std::min<uint64_t>((max_n + kDigestThreads - 1) / kDigestThreads,
                             (uint64_t)per_cu * (uint64_t)c->ncu));
+  if (max_blocks) blocks = std::min<uint64_t>(blocks, max_blocks);
   HIPCHK(c, hipMemsetAsync(queue, 0, 4, stream));
   da.queue = queue;
   da.nfirst = (uint32_t)std::min<uint64_t>(da.n, blocks * kDigestThreads);

@@ -314,7 +314,17 @@ struct dsx_ctx {
   // dsx_index_*'s digests run here, so a window's digest (its longest chunk's
   // chain, ~10-15 ms) does not hold the next window's scans and stitches on
   // `stream` (nor the tail feeder, which follows their published totals)
+  // (= idx_side[0])
   hipStream_t idx_dg_stream = nullptr;
+  // the GPU's shares of a one-window call during its read (dsx_index.cpp), one
+  // stream each so that they run side by side, each with its queue counter
+  // (idx_side_q[32 k], one 128-B line each; [32 kIdxSide]: the last window's
+  // digest on `stream`); lowest priority: the runtime's
+  // low-priority pool of GPU_MAX_HW_QUEUES (4) HSA queues holds exactly these,
+  // none shared with `stream` or `copy_stream` (tools/queue_probe.hip)
+  static constexpr int kIdxSide = 4;
+  hipStream_t idx_side[kIdxSide] = {};
+  DevBuf<uint32_t> idx_side_q;
   hipEvent_t q_ev[kQueueDepth] = {};
   uint32_t q_next = 0;
 };
@@ -372,6 +382,11 @@ void host_parallel(int parts, const std::function<void(int)>& fn);
 // cgroup v2 quota and OMP_NUM_THREADS (the GPU box's per-GPU share), or
 // DSX_HOST_THREADS when set
 int host_cpu_share();
+// a stream for work beside the pipeline (window digests, the tail feeder's
+// copies; dsx_stream.cpp): the lowest priority, so it takes an HSA queue of
+// the runtime's low-priority pool instead of sharing one with the scan or
+// copy stream (GPU_MAX_HW_QUEUES per pool, 4 on the box, tools/queue_probe)
+hipError_t side_stream_create(hipStream_t* s);
 // SHA-512/256 on the host (dsx_hostsha.cpp): one message, or 8 at once in
 // AVX-512 lanes (only when host_sha_vec(); n[i] == UINT64_MAX: unused lane)
 bool host_sha_vec();
@@ -392,8 +407,9 @@ int flush_publish(dsx_ctx* c);  // launch the pending publish, if any
 int launch_stitch(dsx_ctx* c, const CallCfg& cc, const PieceCands& pc, uint64_t P, uint64_t len,
                   bool is_last, uint64_t seq, bool trace);
 // digest_kernel on `stream` (null: the ctx stream) with queue counter `queue`
-// (null: the ctx's); max_n bounds the chunk count (sizes the grid)
+// (null: the ctx's); max_n bounds the chunk count (sizes the grid); pc: 1
+// digest_pc_kernel, 0 digest_kernel, -1 by max_n (DSX_DIGEST_PC overrides)
 int launch_digest(dsx_ctx* c, DigestArgs da, uint64_t max_n, int algo, hipStream_t stream = nullptr,
-                  uint32_t* queue = nullptr, bool serial = false);
+                  uint32_t* queue = nullptr, bool serial = false, uint32_t max_blocks = 0, int pc = -1);
 void index_release(dsx_ctx* c);   // dsx_index.cpp: frees the pipeline's buffers
 void stream_release(dsx_ctx* c);  // dsx_stream.cpp: frees the stream's buffers

@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <deque>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -41,12 +42,16 @@ namespace {
 using FillFn = int (*)(void* ud, uint8_t* dst, uint64_t off, uint64_t n);
 
 // Reads pieces [k*piece, (k+1)*piece) of the source into slot k % K on
-// reader threads, ahead of the consumer, never more than K pieces ahead.
+// reader threads, ahead of the consumer, never more than K pieces ahead; from
+// fine_from on (a multiple of piece) the pieces are `fine` bytes.
 class Prefetcher {
  public:
   Prefetcher(FillFn fill, void* ud, uint64_t len, uint64_t piece, uint8_t* const* slots, int nslots,
-             int nthreads)
-      : fill_(fill), ud_(ud), len_(len), piece_(piece), np_((len + piece - 1) / piece),
+             int nthreads, uint64_t fine_from = UINT64_MAX, uint64_t fine = 0)
+      : fill_(fill), ud_(ud), len_(len), piece_(piece),
+        fine_from_(fine && fine_from < len ? fine_from : UINT64_MAX), fine_(fine ? fine : piece),
+        kf_(fine_from_ < len ? fine_from_ / piece : (len + piece - 1) / piece),
+        np_(kf_ + (fine_from_ < len ? (len - fine_from_ + fine_ - 1) / fine_ : 0)),
         slots_(slots, slots + nslots), have_(nslots, -1), allow_(nslots), rc_(nslots, 0) {
     for (int s = 0; s < nslots; ++s) allow_[s] = s;
     const int nt = std::max(1, std::min<int>(nthreads, (int)std::min<uint64_t>(np_, 64)));
@@ -59,7 +64,7 @@ class Prefetcher {
     std::unique_lock<std::mutex> lk(m_);
     cv_.wait(lk, [&] { return have_[s] == (int64_t)k; });
     *p = slots_[s];
-    *n = std::min(piece_, len_ - k * piece_);
+    *n = plen(k);
     return rc_[s];
   }
   // the slot holding piece k may be refilled (its H2D copy has landed)
@@ -94,8 +99,7 @@ class Prefetcher {
         cv_.wait(lk, [&] { return stop_ || allow_[s] == (int64_t)k; });
         if (stop_) return;
       }
-      const uint64_t off = k * piece_;
-      const int rc = fill_(ud_, slots_[s], off, std::min(piece_, len_ - off));
+      const int rc = fill_(ud_, slots_[s], poff(k), plen(k));
       {
         std::lock_guard<std::mutex> lk(m_);
         rc_[s] = rc;
@@ -104,9 +108,14 @@ class Prefetcher {
       cv_.notify_all();
     }
   }
+  uint64_t poff(uint64_t k) const { return k < kf_ ? k * piece_ : fine_from_ + (k - kf_) * fine_; }
+  uint64_t plen(uint64_t k) const {
+    const uint64_t o = poff(k);
+    return std::min(k < kf_ ? piece_ : fine_, len_ - o);
+  }
   FillFn fill_;
   void* ud_;
-  uint64_t len_, piece_, np_;
+  uint64_t len_, piece_, fine_from_, fine_, kf_, np_;
   std::vector<uint8_t*> slots_;
   std::vector<int64_t> have_, allow_;
   std::vector<int> rc_;
@@ -165,17 +174,21 @@ int index_setup(dsx_ctx* c, uint64_t slot_bytes) {
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : c->idx_stitch_ev)
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (!c->idx_dg_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->idx_dg_stream, hipStreamNonBlocking));
+  for (auto& s : c->idx_side)
+    if (!s) HIPCHK(c, side_stream_create(&s));
+  c->idx_dg_stream = c->idx_side[0];
+  HIPCHK(c, c->idx_side_q.ensure(32 * (dsx_ctx::kIdxSide + 1)));  // (+ the end digest's)
   return DSX_OK;
 }
 
 // A window's digest on the digest stream, after the window's last stitch and
 // snapshot (recorded on `stream`); then the event the copy stream waits for
 // before it refills the window's buffer.
-int launch_window_digest(dsx_ctx* c, const DigestArgs& da, uint64_t max_n, int algo, int slot) {
+int launch_window_digest(dsx_ctx* c, const DigestArgs& da, uint64_t max_n, int algo, int slot,
+                         uint32_t max_blocks = 0) {
   HIPCHK(c, hipEventRecord(c->idx_stitch_ev[slot], c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->idx_dg_stream, c->idx_stitch_ev[slot], 0));
-  const int rc = launch_digest(c, da, max_n, algo, c->idx_dg_stream, nullptr, true);
+  const int rc = launch_digest(c, da, max_n, algo, c->idx_dg_stream, nullptr, true, max_blocks);
   if (rc) return rc;
   HIPCHK(c, hipEventRecord(c->idx_win_ev[slot], c->idx_dg_stream));
   return DSX_OK;
@@ -188,7 +201,8 @@ int drain(dsx_ctx* c, Prefetcher& pf, int rc) {
   (void)hipStreamSynchronize(c->copy_stream);
   (void)hipStreamSynchronize(c->scan_stream);
   (void)hipStreamSynchronize(c->stream);
-  if (c->idx_dg_stream) (void)hipStreamSynchronize(c->idx_dg_stream);
+  for (auto& s : c->idx_side)  // (idx_dg_stream among them)
+    if (s) (void)hipStreamSynchronize(s);
   return rc;
 }
 
@@ -217,12 +231,13 @@ struct ProgressScope {
 // runs at the clock an idle-ish GPU has then, ~58 ns per byte, against ~38 ns
 // on a busy one; 16 host threads read and hash ~43 GB/s)
 constexpr double kGpuNsPerByte = 58.0;   // digest_pc_kernel, one lane, end of a file call
-#if DSX_DIAG
 constexpr double kReadBytesPerNs = 45.0;  // page cache -> HBM through the pinned slots (dsx_cut_fd, ~42 GiB/s)
-#endif
 constexpr double kHostNsPerByte = 0.38;  // one host thread, read + hash (AVX-512)
 constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
 constexpr int kTailThreads = 16;
+constexpr size_t kMaxMids = dsx_ctx::kIdxSide;  // GPU shares of a one-window call during its read
+constexpr uint64_t kFineTail = 32ull << 20;      // the call's last bytes in smaller pieces
+constexpr uint64_t kFineDiv = 4;                 // of piece / kFineDiv bytes
 
 struct TailChunk {
   uint64_t idx, start, len;
@@ -281,15 +296,52 @@ struct TailSrc {
   const uint8_t* direct = nullptr;  // the source's bytes [0, len) in host memory
 };
 
+// Hashes chunks t[0, cnt) (cnt <= 8: one AVX-512 group, else cnt == 1 on the
+// scalar path) into ids[32 j]; their bytes from the caller's memory or read
+// again through `fill` into buf.
+int hash_group(const TailSrc& src, const TailChunk* t, uint64_t cnt, uint8_t* ids,
+               std::vector<uint8_t>& buf) {
+  const bool vec = host_sha_vec();
+  const uint64_t per = vec ? 8 : 1;
+  uint64_t total = 0;
+  for (uint64_t j = 0; j < cnt; ++j) total += t[j].len;
+  if (!src.direct && buf.size() < total + 1) buf.resize(total + 1);
+  const uint8_t* p[8];
+  uint64_t n[8];
+  uint8_t* o[8];
+  uint64_t at = 0;
+  int rc = DSX_OK;
+  for (uint64_t j = 0; j < per; ++j) {
+    if (j >= cnt) {
+      p[j] = nullptr;
+      n[j] = UINT64_MAX;
+      o[j] = nullptr;
+      continue;
+    }
+    n[j] = t[j].len;
+    o[j] = ids + 32 * j;
+    if (src.direct) {
+      p[j] = src.direct + t[j].start;
+      continue;
+    }
+    if (t[j].len && rc == DSX_OK) rc = src.fill(src.ud, buf.data() + at, t[j].start, t[j].len);
+    p[j] = buf.data() + at;
+    at += t[j].len;
+  }
+  if (rc) return rc;
+  if (vec)
+    host_sha512_256_x8(p, n, o);
+  else
+    host_sha512_256_one(p[0], n[0], o[0]);
+  return DSX_OK;
+}
+
 // Stops with DSX_E_INTERRUPTED between groups once `halt` (the caller's: a
 // feeder told to stop, an error path joining it) or `cancel` (dsx_cancel) is
 // set, so a cancelled call does not wait for a whole window's host hash.
 int hash_tail(const TailSrc& src, const std::vector<TailChunk>& t, uint8_t* ids, int threads,
               const std::atomic<int>* halt, const std::atomic<int>* cancel) {
-  const FillFn fill = src.fill;
-  void* const ud = src.ud;
-  const bool vec = host_sha_vec();
-  const uint64_t per = vec ? 8 : 1;
+  const uint64_t per = host_sha_vec() ? 8 : 1;
   const uint64_t groups = (t.size() + per - 1) / per;
   std::atomic<uint64_t> next{0};
   std::atomic<int> err{DSX_OK};
@@ -302,38 +354,7 @@ int hash_tail(const TailSrc& src, const std::vector<TailChunk>& t, uint8_t* ids,
         return;
       }
       const uint64_t j0 = g * per, j1 = std::min<uint64_t>(t.size(), j0 + per);
-      uint64_t total = 0;
-      for (uint64_t j = j0; j < j1; ++j) total += t[j].len;
-      if (buf.size() < total + 1) buf.resize(total + 1);
-      const uint8_t* p[8];
-      uint64_t n[8];
-      uint8_t* o[8];
-      uint64_t at = 0;
-      int rc = DSX_OK;
-      for (uint64_t j = j0; j < j0 + per; ++j) {
-        const int q = (int)(j - j0);
-        if (j >= j1) {
-          p[q] = nullptr;
-          n[q] = UINT64_MAX;
-          o[q] = nullptr;
-          continue;
-        }
-        n[q] = t[j].len;
-        o[q] = ids + 32 * j;
-        if (src.direct) {
-          p[q] = src.direct + t[j].start;
-          continue;
-        }
-        if (t[j].len && rc == DSX_OK) rc = fill(ud, buf.data() + at, t[j].start, t[j].len);
-        p[q] = buf.data() + at;
-        at += t[j].len;
-      }
-      if (rc == DSX_OK) {
-        if (vec)
-          host_sha512_256_x8(p, n, o);
-        else
-          host_sha512_256_one(p[0], n[0], o[0]);
-      }
+      const int rc = hash_group(src, t.data() + j0, j1 - j0, ids + 32 * j0, buf);
       if (rc) {
         err.store(rc);
         return;
@@ -354,11 +375,23 @@ class TailFeeder {
  public:
   // (the last of several windows: start_ev marks the previous window's
   // snapshot dsnap = {cuts before this window, their last end})
-  TailFeeder(dsx_ctx* c, const TailSrc& src, uint64_t len, uint64_t cut, int threads,
+  // (`cut`: the cut of the chunks before the first boundary; a boundary, a
+  // snapshot the GPU hashed the shorter chunks before during the read, sets
+  // the cut of those after it)
+  // (cap: at most this many chunks in the window)
+  TailFeeder(dsx_ctx* c, const TailSrc& src, uint64_t len, uint64_t cut, int threads, uint64_t cap,
              uint64_t seq0, hipEvent_t start_ev = nullptr, const uint64_t* dsnap = nullptr)
-      : c_(c), src_(src), len_(len), cut_(cut), threads_(threads), seq0_(seq0),
+      : c_(c), src_(src), len_(len), cut_(cut), cap_(cap), threads_(threads), seq0_(seq0),
         start_ev_(start_ev), dsnap_(dsnap) {
     th_ = std::thread([this] { run(); });
+  }
+  // a snapshot {total, carry} was enqueued (ev after it): chunks from its
+  // total on take `cut_after`.  Called before the pieces after the snapshot
+  // are enqueued, so no total the feeder reads after it can come from them
+  // without it knowing the boundary.
+  void add_boundary(hipEvent_t ev, const uint64_t* snap, uint64_t cut_after) {
+    std::lock_guard<std::mutex> g(m_);
+    bounds_.push_back({ev, snap, cut_after, 0});
   }
   ~TailFeeder() { stop(); }
   void finish(uint64_t total) {
@@ -375,7 +408,7 @@ class TailFeeder {
     return err_;
   }
   void stop() {
-    halt_.store(1);  // (a batch being hashed ends at its next group of 8)
+    halt_.store(1);  // (the hashers stop at their next group of 8)
     {
       std::lock_guard<std::mutex> g(m_);
       stop_ = true;
@@ -395,78 +428,161 @@ class TailFeeder {
     const uint64_t q1 = h->seq;
     return (q0 == q1 && q0 > seq0_) ? t : 0;
   }
+  // This thread follows the published totals and queues each new batch's
+  // long chunks, longest first, in groups of 8 (part 0 of the host pool);
+  // threads_ more parts hash the groups as they come.  (Until round 6 each
+  // batch was hashed whole before the next was fetched: the threads idled at
+  // every batch's end, and the call's last batch waited for the one before.)
   void run() {
     if (hipSetDevice(c_->device) != hipSuccess) {
       err_ = DSX_E_HIP;
       return;
     }
+    // (normal priority: with the null stream, `stream` and `copy_stream` the
+    // fourth queue of that pool; the low-priority pool is the digests')
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
       err_ = DSX_E_HIP;
       return;
     }
+    chunks.reserve(cap_);  // (never reallocated: the hashers read it while it grows)
+    ids.assign(32 * cap_, 0);
+    const uint64_t per = host_sha_vec() ? 8 : 1;
+    std::mutex qm;
+    std::condition_variable qcv;
+    std::deque<std::pair<size_t, uint64_t>> q;  // {first chunk, count}
+    bool qdone = false;
+    std::atomic<int> herr{DSX_OK};
+    auto fail = [&](int rc) {
+      int ok = DSX_OK;
+      herr.compare_exchange_strong(ok, rc);
+      qcv.notify_all();
+    };
+    host_parallel(threads_ + 1, [&](int part) {
+      if (part == 0) {
+        const int rc = produce(s, [&](std::vector<TailChunk>& batch) -> int {
+          if (chunks.size() + batch.size() > cap_) return DSX_E_INTERNAL;
+          std::sort(batch.begin(), batch.end(),
+                    [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
+          {
+            std::lock_guard<std::mutex> g(qm);
+            const size_t at = chunks.size();
+            chunks.insert(chunks.end(), batch.begin(), batch.end());
+            for (uint64_t j = 0; j < batch.size(); j += per)
+              q.push_back({at + j, std::min<uint64_t>(per, batch.size() - j)});
+          }
+          qcv.notify_all();
+          return herr.load();
+        });
+        if (rc) fail(rc);
+        {
+          std::lock_guard<std::mutex> g(qm);
+          qdone = true;
+        }
+        qcv.notify_all();
+        return;
+      }
+      std::vector<uint8_t> buf;
+      for (;;) {
+        std::pair<size_t, uint64_t> g;
+        {
+          std::unique_lock<std::mutex> lk(qm);
+          qcv.wait(lk, [&] { return !q.empty() || qdone || herr.load() != DSX_OK; });
+          if (herr.load() != DSX_OK || q.empty()) return;
+          g = q.front();
+          q.pop_front();
+        }
+        if (halt_.load(std::memory_order_relaxed) || c_->cancel.load(std::memory_order_relaxed)) {
+          fail(DSX_E_INTERRUPTED);
+          return;
+        }
+        const int rc = hash_group(src_, chunks.data() + g.first, g.second, ids.data() + 32 * g.first, buf);
+        if (rc) {
+          fail(rc);
+          return;
+        }
+      }
+    });
+    ids.resize(32 * chunks.size());
+    if (!err_) err_ = herr.load();
+    (void)hipStreamDestroy(s);
+  }
+  // the follower: each batch of newly final chunks above their cut goes to
+  // `put` (which returns non-zero to stop); returns a HIP error, or OK once
+  // the final count is in
+  template <class Put>
+  int produce(hipStream_t s, Put&& put) {
     std::vector<uint64_t> e;
     uint64_t seen = 0, prev = 0;
     if (start_ev_) {
       uint64_t sn[2] = {0, 0};
       if (hipEventSynchronize(start_ev_) != hipSuccess ||
           hipMemcpyAsync(sn, dsnap_, sizeof sn, hipMemcpyDeviceToHost, s) != hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess) {
-        err_ = DSX_E_HIP;
-        (void)hipStreamDestroy(s);
-        return;
-      }
+          hipStreamSynchronize(s) != hipSuccess)
+        return DSX_E_HIP;
       seen = sn[0];
       prev = sn[1];
     }
+    std::vector<Bound> known;  // the boundaries resolved so far (their totals read)
     while (true) {
       uint64_t target;
       bool last;
+      std::vector<Bound> fresh;
       {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait_for(g, std::chrono::microseconds(200), [&] { return stop_ || have_final_; });
-        if (stop_) break;
+        if (stop_) return DSX_E_INTERRUPTED;
         last = have_final_;
+        // (read with the boundaries under one lock: a total published before
+        // add_boundary cannot come from a piece after that snapshot)
         target = last ? final_ : std::max(seen, published());
+        fresh.assign(bounds_.begin() + (long)known.size(), bounds_.end());
+      }
+      for (Bound& b : fresh) {
+        uint64_t sn[2] = {0, 0};
+        if (hipEventSynchronize(b.ev) != hipSuccess ||
+            hipMemcpyAsync(sn, b.snap, sizeof sn, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+          return DSX_E_HIP;
+        b.total = sn[0];
+        known.push_back(b);
       }
       if (target > seen) {
         e.resize(target - seen);
         if (hipMemcpyAsync(e.data(), c_->out.p + seen, e.size() * 8, hipMemcpyDeviceToHost, s) !=
                 hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-          err_ = DSX_E_HIP;
-          break;
-        }
+            hipStreamSynchronize(s) != hipSuccess)
+          return DSX_E_HIP;
         std::vector<TailChunk> batch;
         for (uint64_t i = 0; i < e.size(); ++i) {
           const uint64_t st = i ? e[i - 1] : prev;
           // (a call that overflows its candidate slots reruns and drops these:
           // never read outside the source for them)
-          if (e[i] > st && e[i] <= len_ && e[i] - st > cut_) batch.push_back({seen + i, st, e[i] - st});
+          uint64_t cut = cut_;
+          for (const Bound& b : known)
+            if (seen + i >= b.total) cut = b.cut_after;
+          if (e[i] > st && e[i] <= len_ && e[i] - st > cut) batch.push_back({seen + i, st, e[i] - st});
         }
         prev = e.back();
         seen = target;
         if (!batch.empty()) {
-          std::sort(batch.begin(), batch.end(),
-                    [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
-          const size_t at = chunks.size();
-          ids.resize(32 * (at + batch.size()));
-          const int rc = hash_tail(src_, batch, ids.data() + 32 * at, threads_, &halt_, &c_->cancel);
-          if (rc) {
-            err_ = rc;
-            break;
-          }
-          chunks.insert(chunks.end(), batch.begin(), batch.end());
+          const int rc = put(batch);
+          if (rc) return rc;
         }
       }
-      if (last) break;
+      if (last) return DSX_OK;
     }
-    (void)hipStreamDestroy(s);
   }
   dsx_ctx* c_;
   TailSrc src_;
   uint64_t len_;
-  uint64_t cut_;
+  uint64_t cut_, cap_;
+  struct Bound {
+    hipEvent_t ev;
+    const uint64_t* snap;
+    uint64_t cut_after, total;
+  };
+  std::vector<Bound> bounds_;  // (add_boundary, under m_)
   int threads_;
   uint64_t seq0_;
   hipEvent_t start_ev_;
@@ -522,11 +638,29 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   if (W >= len) W = (len + piece - 1) / piece * piece;  // one window
   const uint64_t nwin = (len + W - 1) / W;
   const uint64_t scan_step = std::max<uint64_t>(piece, kScanStep / piece * piece);
+  // The file's last kFineTail bytes (in its last window) are read, copied and
+  // scanned in pieces of piece / kFineDiv: the tail feeder then sees the long
+  // chunks of the call's last piece, the host's last batch, a few MB sooner.
+  // (Smaller pieces throughout slow the read: 8 MiB slots, 28 against 45
+  // GiB/s for dsx_cut_fd, profiles/r06ad.)
+  uint64_t fine_tail = kFineTail, fine_div = kFineDiv;
+#if DSX_DIAG
+  if (const char* v = getenv("DSX_FINE_TAIL")) fine_tail = (uint64_t)atol(v);
+  if (const char* v = getenv("DSX_FINE_DIV")) fine_div = std::max<uint64_t>(1, atol(v));
+#endif
+  const uint64_t fine = std::max<uint64_t>(4096, (piece / fine_div) & ~4095ull);
+  uint64_t fine_from = UINT64_MAX;
+  const bool feeds = algo == DSX_DIGEST_SHA512_256 && out_ids &&
+                     (c->index_host_tail > 0 || (c->index_host_tail < 0 && host_sha_vec()));
+  if (feeds && fine_tail && fine < piece) {  // (only the tail feeder gains from them)
+    const uint64_t last_ws = (nwin - 1) * W;
+    fine_from = std::max(last_ws, (len - std::min(len, fine_tail)) / piece * piece);
+  }
   rc = index_setup(c, piece);
   if (rc) return rc;
   HIPCHK(c, grow(c, c->idx_win[0], pre + W));
   if (nwin > 1) HIPCHK(c, grow(c, c->idx_win[1], pre + W));
-  HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 2)));  // (+1: the one window's mid snapshot)
+  HIPCHK(c, grow(c, c->idx_snap, 2 * (nwin + 1 + kMaxMids)));  // (+ the one window's mid snapshots)
   HIPCHK(c, grow(c, c->out, need));
   if (algo >= 0) HIPCHK(c, grow(c, c->dg_ids, need * 32));
   const int K = dsx_ctx::kIdxSlots;
@@ -540,7 +674,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     rc = reset_state(c, 0);
     if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->idx_snap.p, 0, 2 * sizeof(uint64_t), c->stream));  // {0 cuts, cut 0}
-    Prefetcher pf(fill, ud, len, piece, c->idx_slots, K, c->index_readers);
+    Prefetcher pf(fill, ud, len, piece, c->idx_slots, K, c->index_readers, fine_from, fine);
     const TailSrc tsrc{fill, ud, direct};  // (the host tail's bytes)
     uint64_t k = 0;  // piece index
     uint64_t w = 0, ws = 0, wl = 0;
@@ -577,8 +711,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       return err;
     };
     // the host tail of the last window (SHA-512/256 only; auto needs AVX-512)
-    const bool tail_on = algo == DSX_DIGEST_SHA512_256 && out_ids &&
-                         (c->index_host_tail > 0 || (c->index_host_tail < 0 && host_sha_vec()));
+    const bool tail_on = feeds;
     std::vector<TailChunk> tail;
     std::vector<uint8_t> tail_ids;
     // the last window's long chunks are hashed on the host during its read;
@@ -594,30 +727,75 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     std::unique_ptr<TailFeeder> feed;
     const int fth = feed_threads(c);
     const uint64_t fcut = feed_cut(c, fth);
-    // (Diagnostic) one window (a file up to DSX_INDEX_WINDOW): its first `mid` bytes are
-    // hashed on the GPU WHILE the rest is read -- a digest on the digest
-    // stream over the chunks stitched by then, every size (its chain, at most
-    // max bytes, ends before the read does) -- and the tail feeder starts at
-    // that point, so the host hashes only the long chunks after it.  mid is
-    // where the remaining read time covers the longest chain: (1 - mid/len)
-    // x the read time >= max x kGpuNsPerByte, at most half the window.  (The
-    // host, at the process's CPU share, cannot keep up with the long chunks
-    // of a whole window)
-    uint64_t mid_at = 0;
+    // One window (a file up to DSX_INDEX_WINDOW): the GPU hashes most of it
+    // DURING the read.  At the points f_k of the window (1/2, 3/4, ...) a
+    // snapshot follows the piece's stitch and a digest on side stream k (a
+    // "share") hashes the chunks confirmed since the previous point, all but
+    // those longer than cut_k = the read time left after f_k over the GPU's
+    // ns per byte: its chain ends about when the read does.  The feeder
+    // hashes, from the call's start, each segment's chunks above its cut and
+    // the last segment's above fcut_end; the digest after the read (on
+    // `stream`, digest_pc_kernel) takes the last segment's short chunks, a
+    // chain of at most fcut_end bytes.  The points stop where cut_k would
+    // fall below 1.25 x fcut_end (two points at 1 GiB and 12 threads); none
+    // when the first is below 2 x fcut_end (files below ~0.6 GiB), for
+    // SHA-256, or without the host tail.  At 1 GiB and 12 threads the host
+    // takes 2,985 chunks against 6,060 without the shares, and the call
+    // reads 0.87-0.90 x dsx_cut_fd against 0.78-0.84.
+    // The side streams have hardware queues of their own (side_stream_create):
+    // on one shared with the pipeline's streams the shares held the next
+    // pieces' scans and the call fell to 0.58-0.63 x dsx_cut_fd
+    // (profiles/r06q, r06x).  Four shares (down to 7/8 and 15/16) slowed the
+    // read: 0.87 against 0.89 (profiles/r06ag).
+    // (A first form gave the GPU every chunk of the first half and started
+    // the feeder at mid: the host then had less time for the same work, 0.66-
+    // 0.72 x dsx_cut_fd against 0.78, profiles/r06e, r06f.)
+    struct Mid {
+      uint64_t at, cut;
+    };
+    std::vector<Mid> mids;
+    uint64_t fcut_end = fcut;
+    double share_ns = kGpuNsPerByte;  // the shares' chain, ns per byte
+    double slack_ns = 0;              // a share may end this long after the read
+    int share_pc = 1;
 #if DSX_DIAG
-    // (measured, not kept: the host, which then starts at mid, finished
-    // later -- 0.72 x dsx_cut_fd against 0.78 without, profiles/r06e; the
-    // diagnostic build keeps it behind DSX_FEED_MID for the record)
-    if (tail_on && nwin == 1 && getenv("DSX_FEED_MID")) {
-      const double t_read = (double)len / kReadBytesPerNs;     // ns
-      double frac = 1.0 - (double)p->max * kGpuNsPerByte / t_read;
-      frac = std::min(frac, 0.5);
-      frac = std::min(frac, atof(getenv("DSX_FEED_MID")));
-      if (frac >= 0.1) mid_at = (uint64_t)(frac * (double)len);
-    }
+    if (const char* v = getenv("DSX_SHARE_NS")) share_ns = std::max(10.0, atof(v));
+    if (const char* v = getenv("DSX_SHARE_SLACK")) slack_ns = 1e3 * atof(v);  // (us)
+    if (const char* v = getenv("DSX_SHARE_PC")) share_pc = atoi(v);
 #endif
-    uint64_t* const mid_snap = c->idx_snap.p + 2 * (nwin + 1);
-    bool mid_done = false;
+    if (tail_on && nwin == 1 && c->index_host_tail < 0) {
+      // with the shares the host has fewer bytes: 3/4 of the usual cut
+      // after the last point (64 -> 48 KiB at 12 threads; profiles/r06af,
+      // r06ag: 0.882 / 0.898 x dsx_cut_fd against 0.874 / 0.894)
+      fcut_end = std::max<uint64_t>(kFeedCutBase, (fcut * 3 / 4) & ~4095ull);
+      const double t_read = (double)len / kReadBytesPerNs;  // ns
+      std::vector<double> fr;
+      for (double f = 0.5; f < 0.99 && fr.size() < kMaxMids; f = 0.5 * (1.0 + f)) fr.push_back(f);
+#if DSX_DIAG
+      if (const char* v = getenv("DSX_FEED_MID")) {  // (A/B: "0" off, else a list "0.5,0.75")
+        fr.clear();
+        for (const char* q = v; *q && fr.size() < kMaxMids;) {
+          char* nx = nullptr;
+          const double f = strtod(q, &nx);
+          if (nx == q) break;
+          if (f > 0.05 && f < 0.99 && (fr.empty() || f > fr.back())) fr.push_back(f);
+          q = *nx == ',' ? nx + 1 : nx;
+        }
+      }
+      if (const char* v = getenv("DSX_FEED_CUT_END")) fcut_end = std::max<uint64_t>(4096, atol(v));
+#endif
+      for (double f : fr) {
+        const double ck = ((1.0 - f) * t_read + slack_ns) / share_ns;
+        if (ck < (mids.empty() ? 2.0 : 1.25) * (double)fcut_end) break;
+        mids.push_back({(uint64_t)(f * (double)len), std::min<uint64_t>(p->max, (uint64_t)ck & ~4095ull)});
+      }
+      if (mids.empty()) fcut_end = fcut;
+    }
+    std::vector<Ev> mid_ev(mids.size());
+    for (auto& x : mid_ev) HIPCHK(c, hipEventCreateWithFlags(&x.e, hipEventDisableTiming));
+    size_t mids_done = 0;
+    // snapshot k: after the piece at mids[k].at (the window's start is idx_snap[0])
+    auto mid_snap = [&](size_t k) { return c->idx_snap.p + 2 * (nwin + 1 + k); };
     for (w = 0; w < nwin; ++w) {
       ws = w * W;
       wl = std::min(W, len - ws);
@@ -626,9 +804,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #if DSX_DIAG
       if (nwin > 1 && getenv("DSX_FEED_MULTI") && atoi(getenv("DSX_FEED_MULTI")) == 0) feed_on = false;
 #endif
-      if (feed_on && !mid_at) {
-        feed.reset(new TailFeeder(c, tsrc, len, fcut, fth, c->piece_seq,
-                                  nwin > 1 ? feed_ev.e : nullptr, c->idx_snap.p + 2 * w));
+      if (feed_on) {
+        feed.reset(new TailFeeder(c, tsrc, len, mids.empty() ? fcut : mids[0].cut, fth,
+                                  (pre + wl) / p->min + 2, c->piece_seq, nwin > 1 ? feed_ev.e : nullptr,
+                                  c->idx_snap.p + 2 * w));
       }
       // the digest of window w-2 read this buffer; the copy stream waits for it
       if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
@@ -636,10 +815,10 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         HIPCHK(c, hipMemcpyAsync(buf, c->idx_win[(w - 1) & 1].p + W, pre,
                                  hipMemcpyDeviceToDevice, c->copy_stream));
       uint64_t scanned = ws;
-      for (uint64_t off = ws; off < ws + wl; off += piece, ++k) {
+      for (uint64_t off = ws, hn = 0; off < ws + wl; off += hn, ++k) {
         if (c->cancel.load()) return partial(DSX_E_INTERRUPTED);
         uint8_t* hp = nullptr;
-        uint64_t hn = 0;
+        hn = 0;
         rc = pf.wait(k, &hp, &hn);
         if (rc) return partial(rc);
         hipError_t e = hipMemcpyAsync(buf + pre + (off - ws), hp, hn, hipMemcpyHostToDevice,
@@ -651,7 +830,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: H2D"));
         if (k >= 1) pf.release(k - 1);
         const uint64_t end = off + hn;
-        if (end == ws + wl || end - scanned >= scan_step) {
+        if (end == ws + wl || end - scanned >= scan_step || end > fine_from) {
           e = scan_wait(c, c->idx_copy_ev[k % K]);  // (the stitch follows the scan)
           if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: wait"));
           const uint64_t halo = w == 0 ? scanned : pre + (scanned - ws);
@@ -661,12 +840,14 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           c->timing = true;
           if (rc) return drain(c, pf, rc);
           scanned = end;
-          if (mid_at && !mid_done && end >= mid_at && end < len) {
-            // the GPU's share of the one window: chunks [0, mid_snap.total)
-            mid_done = true;
+          if (mids_done < mids.size() && end >= mids[mids_done].at && end < len && feed) {
+            // the GPU's share of segment k: chunks [snap[k-1].total,
+            // snap[k].total) up to its cut, on the digest stream, on 3/4 of
+            // the CUs (the rest keep room for the next pieces' scans)
+            const size_t m = mids_done++;
             hipLaunchKernelGGL(state_snapshot_kernel, dim3(1), dim3(64), 0, c->stream,
-                               (const DevState*)c->state.p, mid_snap);
-            e = hipEventRecord(feed_ev.e, c->stream);
+                               (const DevState*)c->state.p, mid_snap(m));
+            e = hipEventRecord(mid_ev[m].e, c->stream);
             if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
             DigestArgs dm{};
             dm.blob = buf + pre;
@@ -674,15 +855,25 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
             dm.len = end;
             dm.ends = c->out.p;
             dm.ids = c->dg_ids.p;
-            dm.range_lo = c->idx_snap.p;
-            dm.range_hi = mid_snap;
-            rc = launch_window_digest(c, dm, end / p->min + 2, algo, 0);
+            dm.range_lo = m ? mid_snap(m - 1) : c->idx_snap.p;
+            dm.range_hi = mid_snap(m);
+            dm.skip_above = mids[m].cut >= p->max ? 0 : mids[m].cut;
+            // (on side stream m after this stitch: the shares run side by side)
+            hipStream_t ss = c->idx_side[m];
+            e = hipStreamWaitEvent(ss, mid_ev[m].e, 0);
+            if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: wait"));
+            // (digest_pc_kernel: its chain ran ~45 ns/B during the read,
+            // digest_kernel's ~85, profiles/r06aa, r06ab)
+            const uint64_t from = m ? mids[m - 1].at : 0;
+            rc = launch_digest(c, dm, (end - from + 2 * p->max) / p->min + 2, algo, ss,
+                               c->idx_side_q.p + 32 * m, false, (uint32_t)(c->ncu * 3 / 4), share_pc);
             if (rc) return drain(c, pf, rc);
-            feed.reset(new TailFeeder(c, tsrc, len, fcut, fth, c->piece_seq, feed_ev.e, mid_snap));
+            feed->add_boundary(mid_ev[m].e, mid_snap(m), m + 1 < mids.size() ? mids[m + 1].cut : fcut_end);
 #if DSX_DIAG
             if (getenv("DSX_TAIL_LOG"))
-              fprintf(stderr, "index: GPU share of the window up to %.1f MB, %.2f ms into the call\n",
-                      end / 1e6, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
+              fprintf(stderr, "index: GPU share %zu up to %.1f MB (cut %lu), %.2f ms into the call\n",
+                      m, end / 1e6, (unsigned long)mids[m].cut,
+                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call_t0).count());
 #endif
           }
 #if DSX_DIAG
@@ -711,7 +902,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       da.len = w == 0 ? wl : pre + wl;
       da.ends = c->out.p;
       da.ids = c->dg_ids.p;
-      da.range_lo = mid_done ? mid_snap : c->idx_snap.p + 2 * w;  // (after the GPU's share)
+      da.range_lo = mids_done ? mid_snap(mids_done - 1) : c->idx_snap.p + 2 * w;  // (after the GPU's shares)
       da.range_hi = c->idx_snap.p + 2 * (w + 1);
       if (tail_on && w + 1 == nwin) {
         // the window's chunk ends (the stitch is done once the stream is)
@@ -727,8 +918,18 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: tail ends"));
         const int threads = std::max(1, std::min(kTailThreads, host_cpu_share()));
         if (feed) {  // the feeder has the long chunks: the GPU the rest
-          da.skip_above = fcut;
-          rc = launch_window_digest(c, da, (pre + wl) / p->min + 2, algo, (int)(w & 1));
+          // on `stream` after the last stitch (nothing follows it there; the
+          // shares hold the side streams), sized by the count of the
+          // window's chunks up to the cut, so that a window's ~10 K of them
+          // run on digest_pc_kernel (its chain ~38 ns/B at the end of a call,
+          // digest_kernel's ~58; profiles/r06aa)
+          da.skip_above = fcut_end;
+          uint64_t short_n = 0;
+          for (uint64_t i = 0, st = snap[1]; i < ends.size(); st = ends[i++]) short_n += ends[i] - st <= fcut_end;
+          // (its own queue counter: the previous window's digest may still
+          // run on idx_dg_stream with the ctx's)
+          rc = launch_digest(c, da, short_n + 2, algo, c->stream, c->idx_side_q.p + 32 * dsx_ctx::kIdxSide,
+                             false);
           if (rc) return drain(c, pf, rc);
 #if DSX_DIAG
           const auto tf0 = std::chrono::steady_clock::now();
@@ -747,11 +948,14 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
           if (getenv("DSX_TAIL_LOG")) {
             const double hms =
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
-            (void)hipStreamSynchronize(c->idx_dg_stream);
+            (void)hipStreamSynchronize(c->stream);
             const double gms =
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
-            fprintf(stderr, "feed: chunks %lu host %zu (cut %lu) host done %.2f ms, GPU done %.2f ms\n",
-                    (unsigned long)i1, tail.size(), (unsigned long)fcut, hms, gms);
+            for (size_t m = 0; m < mids_done; ++m) (void)hipStreamSynchronize(c->idx_side[m]);
+            const double sms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
+            fprintf(stderr, "feed: chunks %lu host %zu (cut %lu) host done %.2f ms, GPU done %.2f ms, shares done %.2f ms\n",
+                    (unsigned long)i1, tail.size(), (unsigned long)fcut_end, hms, gms, sms);
           }
 #endif
           continue;
@@ -790,6 +994,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     rc = read_state(c, &st);  // (the stitches)
     HIPCHK(c, hipStreamSynchronize(c->copy_stream));
     HIPCHK(c, hipStreamSynchronize(c->idx_dg_stream));  // (the digests)
+    for (size_t m = 0; m < mids_done; ++m) HIPCHK(c, hipStreamSynchronize(c->idx_side[m]));
     if (rc) return rc;
     if (st.err & kErrDense) {  // rare: a lane overflowed its candidate slots
       c->stats.dense_fallbacks++;
@@ -1010,11 +1215,10 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
 }  // namespace
 
 void index_release(dsx_ctx* c) {
-  if (c->idx_dg_stream) {
-    (void)hipStreamSynchronize(c->idx_dg_stream);
-    (void)hipStreamDestroy(c->idx_dg_stream);
-    c->idx_dg_stream = nullptr;
-  }
+  c->idx_dg_stream = nullptr;  // (idx_side[0])
+  for (auto& s : c->idx_side)
+    if (s) (void)hipStreamSynchronize(s), (void)hipStreamDestroy(s), s = nullptr;
+  c->idx_side_q.release();
   for (auto& e : c->idx_stitch_ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   for (auto& s : c->idx_slots) {

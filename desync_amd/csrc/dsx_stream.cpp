@@ -661,6 +661,17 @@ class HostPool {
 };
 }  // namespace
 
+hipError_t side_stream_create(hipStream_t* s) {
+#if DSX_DIAG
+  if (const char* v = getenv("DSX_SIDE_PRIO"))
+    if (atoi(v) == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+#endif
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+}
+
 int host_cpu_share() {
   const int share = [] {
     if (const char* v = getenv("DSX_HOST_THREADS")) {

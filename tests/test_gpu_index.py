@@ -136,6 +136,56 @@ def test_index_host_threads(tmp_path, monkeypatch, threads):
             assert n_host == int(np.sum(lens > 131072))
 
 
+@pytest.mark.parametrize("mib,cut1", [(320, 61440), (640, 126976)])
+def test_index_host_tail_gpu_shares(tmp_path, monkeypatch, mib, cut1):
+    """One window large enough for the GPU's shares during the read (at 1/2,
+    3/4, ... of the window, a digest on the digest stream of the chunks
+    confirmed since the previous point up to that point's cut; the feeder
+    taking each segment's chunks above its cut and the last segment's above
+    the usual cut): every ID is hashlib's, and the host took between the
+    chunks above the first cut and those above the usual cut.  32 host
+    threads -> 28 feeders, cut 28 KiB.  The first cut is the read time after
+    1/2 over the GPU's 58 ns per byte, rounded down to 4 KiB: 320 MiB / 45
+    B/ns -> 61440 (one point: 3/4's would be below 1.5 x 28 KiB); 640 MiB ->
+    126976 (two points)."""
+    import concurrent.futures as cf
+
+    import desync_amd
+    from desync_amd import _lib
+    monkeypatch.setenv("DSX_HOST_THREADS", "32")
+    n = (mib << 20) + 4321
+    data = o.synth_uniform_c(48, 0, n)
+    f = tmp_path / "blob"
+    data.tofile(str(f))
+    ctx = _lib.Context(0)
+    try:
+        fd = os.open(str(f), os.O_RDONLY)
+        try:
+            ends, ids = desync_amd.index_fd(fd, MIN, AVG, MAX, ctx=ctx)
+        finally:
+            os.close(fd)
+        n_host = ctx.stats().host_tail_chunks
+        ends2, ids2 = desync_amd.index_host(data, MIN, AVG, MAX, ctx=ctx)
+    finally:
+        ctx.close()
+    ref = o.chunk_parallel(data, MIN, AVG, MAX, o.default_threads())
+    assert np.array_equal(ends, ref) and np.array_equal(ends2, ref)
+    starts = np.concatenate([[0], ref[:-1]]).astype(np.uint64)
+    mv = memoryview(data)
+
+    def h(i):
+        return hashlib.new("sha512_256", mv[int(starts[i]):int(ref[i])]).digest()
+
+    with cf.ThreadPoolExecutor(o.default_threads()) as pool:
+        want = list(pool.map(h, range(ref.size), chunksize=256))
+    assert [bytes(x) for x in ids] == want
+    assert [bytes(x) for x in ids2] == want
+    avx512 = "avx512f" in open("/proc/cpuinfo").read() and "avx512bw" in open("/proc/cpuinfo").read()
+    if avx512:
+        lens = (ref - starts).astype(np.int64)
+        assert int(np.sum(lens > cut1)) <= n_host < int(np.sum(lens > 28672)), n_host
+
+
 @pytest.mark.parametrize("tail,window", [("65536", 16 << 20), ("0", 16 << 20), ("-1", 16 << 20),
                                          ("100000", None), ("-1", None)])
 def test_index_host_tail(tmp_path, monkeypatch, tail, window):
