@@ -215,8 +215,26 @@ extern "C" int dsx_ctx_create(int device, dsx_ctx_t** out) {
   if (const char* v = getenv("DSX_STITCH_CUS")) c->stitch_cus = std::max(0, std::min(c->ncu / 2, atoi(v)));
   if (const char* v = getenv("DSX_SCAN_MASK")) c->scan_mask = atoi(v) != 0;
 #endif
-  CREATE_STEP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  CREATE_STEP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  // The pipeline's streams at the highest priority: the runtime keeps
+  // GPU_MAX_HW_QUEUES (4 on the box) HSA queues per priority and hands a
+  // stream one at its first launch, sharing a queue once the pool is full,
+  // and a kernel on a shared queue waits for the kernel ahead of it
+  // (tools/queue_probe.hip, profiles/r06w, r06ai).  The default pool holds the
+  // null stream and torch's streams (RCCL's among them: bench.py's N > 1
+  // lanes would queue their scans behind another lane's collective); the
+  // high pool holds the contexts' streams alone (copy_stream takes a queue
+  // only where it is used, the file pipelines), the low pool the index
+  // pipeline's digests (side_stream_create).
+  {
+    int least = 0, greatest = 0;
+    CREATE_STEP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+#if DSX_DIAG
+    if (const char* v = getenv("DSX_CTX_PRIO"))  // (A/B: 0 the default priority)
+      if (atoi(v) == 0) greatest = 0;
+#endif
+    CREATE_STEP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+    CREATE_STEP(hipStreamCreateWithPriority(&c->copy_stream, hipStreamNonBlocking, greatest));
+  }
   c->scan_stream = c->stream;
 #if DSX_DIAG
   if (c->stitch_cus > 0) {

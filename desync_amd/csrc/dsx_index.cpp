@@ -438,8 +438,8 @@ class TailFeeder {
       err_ = DSX_E_HIP;
       return;
     }
-    // (normal priority: with the null stream, `stream` and `copy_stream` the
-    // fourth queue of that pool; the low-priority pool is the digests')
+    // (default priority: beside the null stream in that pool; `stream` and
+    // `copy_stream` are in the high pool, the digests in the low one)
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
       err_ = DSX_E_HIP;
@@ -595,6 +595,44 @@ class TailFeeder {
   uint64_t final_ = 0;
   int err_ = DSX_OK;
 };
+// The GPU's shares of a one-window call during its read (run_index,
+// run_ids): the points f_k = 1/2, 3/4, ... of the window where a digest on side
+// stream k hashes the chunks completed since the previous point up to cut_k =
+// the read time left after f_k over the GPU's ns per byte (its chain ends
+// about when the read does).  They stop where cut_k falls below 1.25 x the
+// cut after the last point (`end_cut`); none when the first is below 2 x it.
+struct Mid {
+  uint64_t at, cut;
+};
+std::vector<Mid> plan_shares(uint64_t len, uint64_t max_chunk, uint64_t end_cut) {
+  double share_ns = kGpuNsPerByte;  // the shares' chain, ns per byte
+  double slack_ns = 0;              // a share may end this long after the read
+  const double t_read = (double)len / kReadBytesPerNs;  // ns
+  std::vector<double> fr;
+  for (double f = 0.5; f < 0.99 && fr.size() < kMaxMids; f = 0.5 * (1.0 + f)) fr.push_back(f);
+#if DSX_DIAG
+  if (const char* v = getenv("DSX_SHARE_NS")) share_ns = std::max(10.0, atof(v));
+  if (const char* v = getenv("DSX_SHARE_SLACK")) slack_ns = 1e3 * atof(v);  // (us)
+  if (const char* v = getenv("DSX_FEED_MID")) {  // (A/B: "0" off, else a list "0.5,0.75")
+    fr.clear();
+    for (const char* q = v; *q && fr.size() < kMaxMids;) {
+      char* nx = nullptr;
+      const double f = strtod(q, &nx);
+      if (nx == q) break;
+      if (f > 0.05 && f < 0.99 && (fr.empty() || f > fr.back())) fr.push_back(f);
+      q = *nx == ',' ? nx + 1 : nx;
+    }
+  }
+#endif
+  std::vector<Mid> mids;
+  for (double f : fr) {
+    const double ck = ((1.0 - f) * t_read + slack_ns) / share_ns;
+    if (ck < (mids.empty() ? 2.0 : 1.25) * (double)end_cut) break;
+    mids.push_back({(uint64_t)(f * (double)len), std::min<uint64_t>(max_chunk, (uint64_t)ck & ~4095ull)});
+  }
+  return mids;
+}
+
 // The host's share of the tail: feed_threads() SHA threads beside the
 // readers, within the process's CPU share (host_cpu_share: 16 on the GPU box,
 // whose affinity mask shows the whole machine); the GPU keeps the chunks up
@@ -750,45 +788,21 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     // (A first form gave the GPU every chunk of the first half and started
     // the feeder at mid: the host then had less time for the same work, 0.66-
     // 0.72 x dsx_cut_fd against 0.78, profiles/r06e, r06f.)
-    struct Mid {
-      uint64_t at, cut;
-    };
-    std::vector<Mid> mids;
     uint64_t fcut_end = fcut;
-    double share_ns = kGpuNsPerByte;  // the shares' chain, ns per byte
-    double slack_ns = 0;              // a share may end this long after the read
     int share_pc = 1;
 #if DSX_DIAG
-    if (const char* v = getenv("DSX_SHARE_NS")) share_ns = std::max(10.0, atof(v));
-    if (const char* v = getenv("DSX_SHARE_SLACK")) slack_ns = 1e3 * atof(v);  // (us)
     if (const char* v = getenv("DSX_SHARE_PC")) share_pc = atoi(v);
 #endif
+    std::vector<Mid> mids;
     if (tail_on && nwin == 1 && c->index_host_tail < 0) {
       // with the shares the host has fewer bytes: 3/4 of the usual cut
       // after the last point (64 -> 48 KiB at 12 threads; profiles/r06af,
       // r06ag: 0.882 / 0.898 x dsx_cut_fd against 0.874 / 0.894)
       fcut_end = std::max<uint64_t>(kFeedCutBase, (fcut * 3 / 4) & ~4095ull);
-      const double t_read = (double)len / kReadBytesPerNs;  // ns
-      std::vector<double> fr;
-      for (double f = 0.5; f < 0.99 && fr.size() < kMaxMids; f = 0.5 * (1.0 + f)) fr.push_back(f);
 #if DSX_DIAG
-      if (const char* v = getenv("DSX_FEED_MID")) {  // (A/B: "0" off, else a list "0.5,0.75")
-        fr.clear();
-        for (const char* q = v; *q && fr.size() < kMaxMids;) {
-          char* nx = nullptr;
-          const double f = strtod(q, &nx);
-          if (nx == q) break;
-          if (f > 0.05 && f < 0.99 && (fr.empty() || f > fr.back())) fr.push_back(f);
-          q = *nx == ',' ? nx + 1 : nx;
-        }
-      }
       if (const char* v = getenv("DSX_FEED_CUT_END")) fcut_end = std::max<uint64_t>(4096, atol(v));
 #endif
-      for (double f : fr) {
-        const double ck = ((1.0 - f) * t_read + slack_ns) / share_ns;
-        if (ck < (mids.empty() ? 2.0 : 1.25) * (double)fcut_end) break;
-        mids.push_back({(uint64_t)(f * (double)len), std::min<uint64_t>(p->max, (uint64_t)ck & ~4095ull)});
-      }
+      mids = plan_shares(len, p->max, fcut_end);
       if (mids.empty()) fcut_end = fcut;
     }
     std::vector<Ev> mid_ev(mids.size());
@@ -1113,11 +1127,67 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       if (t.joinable()) t.join();
     }
   } early_th;
+  // One window: the GPU's shares during the read (plan_shares, as in
+  // run_index; here the chunk ranges are known on the host: share k takes the
+  // chunks that end in the pieces landed by its point, up to its cut), and
+  // the host the longer ones from the call's start, with the last segment's
+  // above end_cut -- the lowest cut whose host bytes the threads finish within
+  // ~3/4 of the read (the list is known, so the host can start on the last
+  // segment at once); the digest after the read takes the rest, a chain of
+  // at most end_cut bytes.
+  struct IdShare {
+    uint64_t landed, cut, i1;  // chunks [previous i1, i1) end at or before `landed`
+  };
+  std::vector<IdShare> shares;
+  uint64_t end_cut = early_cut;
+  if (tail_on && nwin == 1 && c->index_host_tail < 0) {
+    for (const Mid& m : plan_shares(L, maxc, early_cut * 3 / 4)) {
+      const uint64_t landed = std::min(L, (m.at + piece - 1) / piece * piece);
+      if (landed >= L) break;
+      uint64_t i1 = shares.empty() ? 0 : shares.back().i1;
+      while (i1 < n && ends[i1] - start <= landed) ++i1;
+      shares.push_back({landed, m.cut, i1});
+    }
+    if (!shares.empty()) {
+      // host bytes: each segment's chunks above its cut, and the last
+      // segment's above end_cut
+      uint64_t fixed = 0;
+      std::vector<uint64_t> last;
+      for (uint64_t i = 0, k = 0; i < n; ++i) {
+        while (k < shares.size() && i >= shares[k].i1) ++k;
+        const uint64_t ln = ends[i] - (i ? ends[i - 1] : start);
+        if (k < shares.size()) {
+          if (ln > shares[k].cut) fixed += ln;
+        } else {
+          last.push_back(ln);
+        }
+      }
+      std::sort(last.begin(), last.end());
+      const double budget = 0.75 * (double)L / kReadBytesPerNs * eth / kHostNsPerByte;  // bytes
+      // the lowest cut (4 KiB steps up to early_cut) whose host bytes fit
+      uint64_t tail_bytes = 0;
+      for (uint64_t x : last) tail_bytes += x;
+      size_t j = 0;
+      end_cut = early_cut;
+      for (uint64_t cut = 4096; cut <= early_cut; cut += 4096) {
+        while (j < last.size() && last[j] <= cut) tail_bytes -= last[j++];
+        if ((double)(fixed + tail_bytes) <= budget) {
+          end_cut = cut;
+          break;
+        }
+      }
+#if DSX_DIAG
+      if (const char* v = getenv("DSX_FEED_CUT_END")) end_cut = std::max<uint64_t>(4096, atol(v));
+#endif
+    }
+  }
   if (tail_on) {
     const uint64_t last_ws = (nwin - 1) * W;  // (the last window: chunks ending past it)
-    for (uint64_t i = 0; i < n; ++i) {
+    for (uint64_t i = 0, k = 0; i < n; ++i) {
       const uint64_t s0 = i ? ends[i - 1] - start : 0, e0 = ends[i] - start;
-      if ((nwin == 1 || e0 > last_ws) && e0 - s0 > early_cut) early.push_back({i, s0, e0 - s0});
+      while (k < shares.size() && i >= shares[k].i1) ++k;
+      const uint64_t cut = k < shares.size() ? shares[k].cut : (shares.empty() ? early_cut : end_cut);
+      if ((nwin == 1 || e0 > last_ws) && e0 - s0 > cut) early.push_back({i, s0, e0 - s0});
     }
     std::sort(early.begin(), early.end(), [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
     early_ids.assign(32 * early.size(), 0);
@@ -1127,6 +1197,7 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
         early_rc = hash_tail(esrc, early, early_ids.data(), eth, &early_th.halt, &c->cancel);
       });
   }
+  size_t shares_done = 0;
   for (uint64_t w = 0; w < nwin; ++w) {
     const uint64_t ws = w * W, wl = std::min(W, L - ws);
     uint8_t* buf = c->idx_win[w & 1].p;
@@ -1146,6 +1217,28 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       if (e == hipSuccess && k >= 1) e = hipEventSynchronize(c->idx_copy_ev[(k - 1) % K]);
       if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: H2D"));
       if (k >= 1) pf.release(k - 1);
+      if (shares_done < shares.size() && off + hn >= shares[shares_done].landed) {
+        // share m: its chunks' bytes have landed once this copy has
+        const size_t m = shares_done++;
+        const uint64_t a = m ? shares[m - 1].i1 : 0, b = shares[m].i1;
+        if (b > a) {
+          hipStream_t ss = c->idx_side[m];
+          e = hipStreamWaitEvent(ss, c->idx_copy_ev[k % K], 0);
+          if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: wait"));
+          DigestArgs dm{};
+          dm.blob = buf + pre;
+          dm.base_off = 0;
+          dm.len = shares[m].landed;
+          dm.ends = c->dg_ends.p + a;
+          dm.first_start = a == 0 ? 0 : ends[a - 1] - start;
+          dm.n = b - a;
+          dm.ids = c->dg_ids.p + a * 32;
+          dm.skip_above = shares[m].cut >= maxc ? 0 : shares[m].cut;
+          rc = launch_digest(c, dm, b - a, algo, ss, c->idx_side_q.p + 32 * m, false,
+                             (uint32_t)(c->ncu * 3 / 4), 1);
+          if (rc) return drain(c, pf, rc);
+        }
+      }
     }
     // chunks ending in (ws, ws + wl] (window 0 also those ending at 0)
     uint64_t i1 = i0;
@@ -1165,7 +1258,15 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       da.ids = c->dg_ids.p + i0 * 32;
       if (tail_on && w + 1 == nwin) {
         da.skip_above = early_cut;
-        rc = launch_digest(c, da, i1 - i0, algo);
+        if (!shares.empty()) {  // (one window: the chunks after the last share)
+          const uint64_t a = shares.back().i1;
+          da.ends = c->dg_ends.p + a;
+          da.first_start = a == 0 ? 0 : ends[a - 1] - start;
+          da.n = i1 - a;
+          da.ids = c->dg_ids.p + a * 32;
+          da.skip_above = end_cut;
+        }
+        if (da.n) rc = launch_digest(c, da, da.n, algo);
         if (rc) return drain(c, pf, rc);
 #if DSX_DIAG
         t_read = t_join0 = ms();
@@ -1195,6 +1296,7 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   }
   pf.stop();
   HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+  for (size_t m = 0; m < shares_done; ++m) HIPCHK(c, hipStreamSynchronize(c->idx_side[m]));
   HIPCHK(c, hipMemcpyAsync(out_ids, c->dg_ids.p, n * 32, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
 #if DSX_DIAG
@@ -1202,9 +1304,9 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
     uint64_t hb = 0;
     for (const auto& x : tail) hb += x.len;
     fprintf(stderr, "ids: %.1f MB windows %lu reads+H2D done %.2f ms, early hash joined %.2f ms "
-            "(waited %.2f; %zu chunks %.1f MB on %d threads, cut %lu), GPU done %.2f ms\n",
+            "(waited %.2f; %zu chunks %.1f MB on %d threads, cut %lu, %zu shares, end cut %lu), GPU done %.2f ms\n",
             L / 1e6, (unsigned long)nwin, t_read, t_join1, t_join1 - t_join0, tail.size(), hb / 1e6, eth,
-            (unsigned long)early_cut, ms());
+            (unsigned long)early_cut, shares.size(), (unsigned long)end_cut, ms());
   }
 #endif
   for (size_t j = 0; j < tail.size(); ++j)  // (the GPU skipped these)

@@ -166,6 +166,15 @@ def test_index_host_tail_gpu_shares(tmp_path, monkeypatch, mib, cut1):
             os.close(fd)
         n_host = ctx.stats().host_tail_chunks
         ends2, ids2 = desync_amd.index_host(data, MIN, AVG, MAX, ctx=ctx)
+        # VerifyIndex of the same list (run_ids' shares: the chunk ranges known
+        # on the host, the last segment's chunks above a budgeted cut on the
+        # host from the call's start)
+        fd = os.open(str(f), os.O_RDONLY)
+        try:
+            vids = desync_amd.ids_fd(fd, 0, ends, ctx=ctx)
+        finally:
+            os.close(fd)
+        vids2 = desync_amd.ids_host(data, 0, ends, ctx=ctx)
     finally:
         ctx.close()
     ref = o.chunk_parallel(data, MIN, AVG, MAX, o.default_threads())
@@ -180,6 +189,8 @@ def test_index_host_tail_gpu_shares(tmp_path, monkeypatch, mib, cut1):
         want = list(pool.map(h, range(ref.size), chunksize=256))
     assert [bytes(x) for x in ids] == want
     assert [bytes(x) for x in ids2] == want
+    assert [bytes(x) for x in vids] == want
+    assert [bytes(x) for x in vids2] == want
     avx512 = "avx512f" in open("/proc/cpuinfo").read() and "avx512bw" in open("/proc/cpuinfo").read()
     if avx512:
         lens = (ref - starts).astype(np.int64)

@@ -77,6 +77,39 @@ def main():
                     name = c.split("=")[0]
                     if os.environ.get("DSX_TAIL_LOG"):  # (the library's log lines follow)
                         print("case: %s" % name, file=sys.stderr, flush=True)
+                    # (`_nomid` in the name: no GPU share of a one-window file
+                    # during the read, DSX_FEED_MID=0 in the diagnostic build;
+                    # `_mK`: the shares at the first K points 1/2, 3/4, 7/8, ...;
+                    # `_eN`: the last segment's cut N KiB, DSX_FEED_CUT_END;
+                    # `_nX`: the shares' cuts at X ns per byte, DSX_SHARE_NS;
+                    # `_k0`: the shares on digest_kernel, DSX_SHARE_PC=0;
+                    # `_tN`: the last N MiB in finer pieces, DSX_FINE_TAIL, 0 off;
+                    # `_dN`: of slot / N bytes, DSX_FINE_DIV;
+                    # `_sN`: the shares may end N us after the read, DSX_SHARE_SLACK)
+                    for v in ("DSX_FEED_MID", "DSX_FEED_CUT_END", "DSX_SHARE_NS", "DSX_SHARE_PC",
+                              "DSX_FINE_TAIL", "DSX_FINE_DIV", "DSX_SHARE_SLACK"):
+                        os.environ.pop(v, None)
+                    for part in name.split("_")[1:]:
+                        if part == "nomid":
+                            os.environ["DSX_FEED_MID"] = "0"
+                        elif part[:1] == "m" and part[1:].isdigit():
+                            pts, f = [], 0.5
+                            for _ in range(int(part[1:])):
+                                pts.append(repr(f))
+                                f = 0.5 * (1 + f)
+                            os.environ["DSX_FEED_MID"] = ",".join(pts) or "0"
+                        elif part[:1] == "e" and part[1:].isdigit():
+                            os.environ["DSX_FEED_CUT_END"] = str(int(part[1:]) << 10)
+                        elif part[:1] == "n" and part[1:].isdigit():
+                            os.environ["DSX_SHARE_NS"] = part[1:]
+                        elif part[:1] == "t" and part[1:].isdigit():
+                            os.environ["DSX_FINE_TAIL"] = str(int(part[1:]) << 20)
+                        elif part[:1] == "d" and part[1:].isdigit():
+                            os.environ["DSX_FINE_DIV"] = part[1:]
+                        elif part[:1] == "s" and part[1:].isdigit():
+                            os.environ["DSX_SHARE_SLACK"] = part[1:]
+                        elif part[:1] == "k" and part[1:].isdigit():
+                            os.environ["DSX_SHARE_PC"] = part[1:]
                     if c.startswith("cut"):
                         t0 = time.perf_counter()
                         desync_amd.cut_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
@@ -88,40 +121,6 @@ def main():
                         os.environ["DSX_FEED_THREADS"] = c.split("=")[1].split(":")[0]
                         # (a name ending in `_nomulti`: no feeder on the last of several windows)
                         os.environ["DSX_FEED_MULTI"] = "0" if name.endswith("_nomulti") else "1"
-                        # (`_nomid` in the name: no GPU share of a one-window file
-                        # during the read, DSX_FEED_MID=0 in the diagnostic build;
-                        # `_mK`: the shares at the first K points 1/2, 3/4, 7/8, ...;
-                        # `_eN`: the last segment's cut N KiB, DSX_FEED_CUT_END)
-                        parts = name.split("_")[1:]
-                        # (`_nX`: the shares' cuts at X ns per byte, DSX_SHARE_NS;
-                        # `_k0`: the shares on digest_kernel, DSX_SHARE_PC=0)
-                        # (`_tN`: the last N MiB in finer pieces, DSX_FINE_TAIL, 0 off;
-                        # `_dN`: of slot / N bytes, DSX_FINE_DIV)
-                        # (`_sN`: the shares may end N us after the read, DSX_SHARE_SLACK)
-                        for v in ("DSX_FEED_MID", "DSX_FEED_CUT_END", "DSX_SHARE_NS", "DSX_SHARE_PC",
-                                  "DSX_FINE_TAIL", "DSX_FINE_DIV", "DSX_SHARE_SLACK"):
-                            os.environ.pop(v, None)
-                        for part in parts:
-                            if part == "nomid":
-                                os.environ["DSX_FEED_MID"] = "0"
-                            elif part[:1] == "m" and part[1:].isdigit():
-                                pts, f = [], 0.5
-                                for _ in range(int(part[1:])):
-                                    pts.append(repr(f))
-                                    f = 0.5 * (1 + f)
-                                os.environ["DSX_FEED_MID"] = ",".join(pts) or "0"
-                            elif part[:1] == "e" and part[1:].isdigit():
-                                os.environ["DSX_FEED_CUT_END"] = str(int(part[1:]) << 10)
-                            elif part[:1] == "n" and part[1:].isdigit():
-                                os.environ["DSX_SHARE_NS"] = part[1:]
-                            elif part[:1] == "t" and part[1:].isdigit():
-                                os.environ["DSX_FINE_TAIL"] = str(int(part[1:]) << 20)
-                            elif part[:1] == "d" and part[1:].isdigit():
-                                os.environ["DSX_FINE_DIV"] = part[1:]
-                            elif part[:1] == "s" and part[1:].isdigit():
-                                os.environ["DSX_SHARE_SLACK"] = part[1:]
-                            elif part[:1] == "k" and part[1:].isdigit():
-                                os.environ["DSX_SHARE_PC"] = part[1:]
                         t0 = time.perf_counter()
                         desync_amd.index_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
                     times[name] = time.perf_counter() - t0

@@ -47,11 +47,19 @@ int main(int argc, char** argv) {
   // prio 1: the last stream at the lowest priority; 2: also the first at the
   // highest (ROCclr keeps a queue pool per priority)
   const int prio = argc > 3 ? atoi(argv[3]) : 0;
+  // idle: streams created first (at the default priority) and never used, as
+  // torch's stream pool creates 32 at once; do they take queues?
+  const int idle = argc > 4 ? atoi(argv[4]) : 0;
+  // prio 3: every measured stream at the highest priority
+  std::vector<hipStream_t> pool(idle);
+  for (auto& x : pool) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   int least = 0, greatest = 0;
   CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   std::vector<hipStream_t> s(nstreams);
   for (int i = 0; i < nstreams; ++i) {
-    if (prio >= 1 && i == nstreams - 1)
+    if (prio == 3)
+      CK(hipStreamCreateWithPriority(&s[i], hipStreamNonBlocking, greatest));
+    else if (prio >= 1 && i == nstreams - 1)
       CK(hipStreamCreateWithPriority(&s[i], hipStreamNonBlocking, least));
     else if (prio >= 2 && i == 0)
       CK(hipStreamCreateWithPriority(&s[i], hipStreamNonBlocking, greatest));
@@ -63,8 +71,8 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   // memrealtime runs at 100 MHz: 20 ms = 2,000,000 ticks
   const unsigned long long ticks = 2000000ull;
-  printf("{\"GPU_MAX_HW_QUEUES\": \"%s\", \"streams\": %d, \"null_touched\": %d, \"prio\": %d, \"drain_ms\": [",
-         q ? q : "", nstreams, (int)touch_null, prio);
+  printf("{\"GPU_MAX_HW_QUEUES\": \"%s\", \"streams\": %d, \"null_touched\": %d, \"prio\": %d, \"idle\": %d, \"drain_ms\": [",
+         q ? q : "", nstreams, (int)touch_null, prio, idle);
   for (int victim = 0; victim < nstreams; ++victim) {
     // spin on the victim stream, then short kernels on each other stream
     hipLaunchKernelGGL(spin, dim3(1), dim3(64), 0, s[victim], d + 1024, ticks);
@@ -97,6 +105,7 @@ int main(int argc, char** argv) {
   }
   printf("]}\n");
   for (auto& x : s) CK(hipStreamDestroy(x));
+  for (auto& x : pool) CK(hipStreamDestroy(x));
   CK(hipFree(d));
   return 0;
 }
