@@ -302,7 +302,10 @@ int dsx_shard_resolve_async(dsx_ctx_t *ctx, const dsx_seam_t *all, int nranks, i
 int dsx_shard_collect(dsx_ctx_t *ctx, dsx_seam_t *my_seam, const int32_t *d_agreed,
                       int32_t *agreed, uint64_t *n_out);
 /* The ctx's HIP stream (hipStream_t), for ordering a caller's collectives
- * with the library's kernels without host waits. */
+ * with the library's kernels without host waits.  It is created at the
+ * highest stream priority, so it takes an HSA queue of that priority's pool
+ * (a caller's streams and RCCL's, at the default priority, do not share it;
+ * DESIGN.md 5.1). */
 int dsx_ctx_stream(dsx_ctx_t *ctx, void **stream);
 
 /* Synchronous copy of n bytes between any host / device pointers (hipMemcpy
