@@ -378,11 +378,13 @@ class TailFeeder {
   // (`cut`: the cut of the chunks before the first boundary; a boundary, a
   // snapshot the GPU hashed the shorter chunks before during the read, sets
   // the cut of those after it)
-  // (cap: at most this many chunks in the window)
+  // (cap: at most this many chunks in the window; extra: hashers that join
+  // once reads_done() -- the readers' CPUs)
   TailFeeder(dsx_ctx* c, const TailSrc& src, uint64_t len, uint64_t cut, int threads, uint64_t cap,
-             uint64_t seq0, hipEvent_t start_ev = nullptr, const uint64_t* dsnap = nullptr)
-      : c_(c), src_(src), len_(len), cut_(cut), cap_(cap), threads_(threads), seq0_(seq0),
-        start_ev_(start_ev), dsnap_(dsnap) {
+             uint64_t seq0, hipEvent_t start_ev = nullptr, const uint64_t* dsnap = nullptr,
+             int extra = 0)
+      : c_(c), src_(src), len_(len), cut_(cut), cap_(cap), threads_(threads), extra_(extra),
+        seq0_(seq0), start_ev_(start_ev), dsnap_(dsnap) {
     th_ = std::thread([this] { run(); });
   }
   // a snapshot {total, carry} was enqueued (ev after it): chunks from its
@@ -394,6 +396,8 @@ class TailFeeder {
     bounds_.push_back({ev, snap, cut_after, 0});
   }
   ~TailFeeder() { stop(); }
+  // the call's reads are done: the extra hashers start
+  void reads_done() { reads_done_.store(1); }
   void finish(uint64_t total) {
     {
       std::lock_guard<std::mutex> g(m_);
@@ -458,7 +462,7 @@ class TailFeeder {
       herr.compare_exchange_strong(ok, rc);
       qcv.notify_all();
     };
-    host_parallel(threads_ + 1, [&](int part) {
+    host_parallel(threads_ + 1 + extra_, [&](int part) {
       if (part == 0) {
         const int rc = produce(s, [&](std::vector<TailChunk>& batch) -> int {
           if (chunks.size() + batch.size() > cap_) return DSX_E_INTERNAL;
@@ -483,6 +487,11 @@ class TailFeeder {
         return;
       }
       std::vector<uint8_t> buf;
+      if (part > threads_) {  // (the readers' CPUs: only once the reads are done)
+        std::unique_lock<std::mutex> lk(qm);
+        while (!reads_done_.load() && !qdone && herr.load() == DSX_OK)
+          qcv.wait_for(lk, std::chrono::microseconds(200));
+      }
       for (;;) {
         std::pair<size_t, uint64_t> g;
         {
@@ -583,7 +592,8 @@ class TailFeeder {
     uint64_t cut_after, total;
   };
   std::vector<Bound> bounds_;  // (add_boundary, under m_)
-  int threads_;
+  int threads_, extra_;
+  std::atomic<int> reads_done_{0};
   uint64_t seq0_;
   hipEvent_t start_ev_;
   const uint64_t* dsnap_;
@@ -765,6 +775,11 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     std::unique_ptr<TailFeeder> feed;
     const int fth = feed_threads(c);
     const uint64_t fcut = feed_cut(c, fth);
+    // the readers' CPUs join the feeder's hashers once the reads are done
+    int feed_extra = std::max(0, std::min(c->index_readers, host_cpu_share() - fth));
+#if DSX_DIAG
+    if (const char* v = getenv("DSX_FEED_EXTRA")) feed_extra = std::max(0, std::min(16, atoi(v)));
+#endif
     // One window (a file up to DSX_INDEX_WINDOW): the GPU hashes most of it
     // DURING the read.  At the points f_k of the window (1/2, 3/4, ...) a
     // snapshot follows the piece's stitch and a digest on side stream k (a
@@ -821,7 +836,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
       if (feed_on) {
         feed.reset(new TailFeeder(c, tsrc, len, mids.empty() ? fcut : mids[0].cut, fth,
                                   (pre + wl) / p->min + 2, c->piece_seq, nwin > 1 ? feed_ev.e : nullptr,
-                                  c->idx_snap.p + 2 * w));
+                                  c->idx_snap.p + 2 * w, feed_extra));
       }
       // the digest of window w-2 read this buffer; the copy stream waits for it
       if (w >= 2) HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->idx_win_ev[w & 1], 0));
@@ -835,6 +850,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
         hn = 0;
         rc = pf.wait(k, &hp, &hn);
         if (rc) return partial(rc);
+        if (feed && off + hn == len) feed->reads_done();  // (the readers are idle now)
         hipError_t e = hipMemcpyAsync(buf + pre + (off - ws), hp, hn, hipMemcpyHostToDevice,
                                       c->copy_stream);
         if (e == hipSuccess) e = hipEventRecord(c->idx_copy_ev[k % K], c->copy_stream);
