@@ -231,6 +231,7 @@ struct ProgressScope {
 // runs at the clock an idle-ish GPU has then, ~58 ns per byte, against ~38 ns
 // on a busy one; 16 host threads read and hash ~43 GB/s)
 constexpr double kGpuNsPerByte = 58.0;   // digest_pc_kernel, one lane, end of a file call
+constexpr double kShareNsPerByte = 45.0;  // the same beside the read's scans (37-40, r06an)
 constexpr double kReadBytesPerNs = 45.0;  // page cache -> HBM through the pinned slots (dsx_cut_fd, ~42 GiB/s)
 constexpr double kHostNsPerByte = 0.38;  // one host thread, read + hash (AVX-512)
 constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
@@ -609,13 +610,17 @@ class TailFeeder {
 // run_ids): the points f_k = 1/2, 3/4, ... of the window where a digest on side
 // stream k hashes the chunks completed since the previous point up to cut_k =
 // the read time left after f_k over the GPU's ns per byte (its chain ends
-// about when the read does).  They stop where cut_k falls below 1.25 x the
-// cut after the last point (`end_cut`); none when the first is below 2 x it.
+// about when the read does; digest_pc_kernel beside the scans ran 37-40 ns
+// per byte, profiles/r06an, so 45 with a margin: 0.892 against 0.872 x
+// dsx_cut_fd at 58, profiles/r06ao).  They stop where cut_k falls below 1.5 x
+// `feed_cut`, the host's usual cut (two points at 1 GiB and 12 threads; a
+// third slowed the read, r06ab, r06am, r06ao); none when the first is below
+// 2 x it.
 struct Mid {
   uint64_t at, cut;
 };
-std::vector<Mid> plan_shares(uint64_t len, uint64_t max_chunk, uint64_t end_cut) {
-  double share_ns = kGpuNsPerByte;  // the shares' chain, ns per byte
+std::vector<Mid> plan_shares(uint64_t len, uint64_t max_chunk, uint64_t feed_cut) {
+  double share_ns = kShareNsPerByte;  // the shares' chain, ns per byte
   double slack_ns = 0;              // a share may end this long after the read
   const double t_read = (double)len / kReadBytesPerNs;  // ns
   std::vector<double> fr;
@@ -637,7 +642,7 @@ std::vector<Mid> plan_shares(uint64_t len, uint64_t max_chunk, uint64_t end_cut)
   std::vector<Mid> mids;
   for (double f : fr) {
     const double ck = ((1.0 - f) * t_read + slack_ns) / share_ns;
-    if (ck < (mids.empty() ? 2.0 : 1.25) * (double)end_cut) break;
+    if (ck < (mids.empty() ? 2.0 : 1.5) * (double)feed_cut) break;
     mids.push_back({(uint64_t)(f * (double)len), std::min<uint64_t>(max_chunk, (uint64_t)ck & ~4095ull)});
   }
   return mids;
@@ -785,13 +790,13 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     // snapshot follows the piece's stitch and a digest on side stream k (a
     // "share") hashes the chunks confirmed since the previous point, all but
     // those longer than cut_k = the read time left after f_k over the GPU's
-    // ns per byte: its chain ends about when the read does.  The feeder
+    // ns per byte (plan_shares): its chain ends about when the read does.  The feeder
     // hashes, from the call's start, each segment's chunks above its cut and
     // the last segment's above fcut_end; the digest after the read (on
     // `stream`, digest_pc_kernel) takes the last segment's short chunks, a
     // chain of at most fcut_end bytes.  The points stop where cut_k would
-    // fall below 1.25 x fcut_end (two points at 1 GiB and 12 threads); none
-    // when the first is below 2 x fcut_end (files below ~0.6 GiB), for
+    // fall below 1.5 x fcut (two points at 1 GiB and 12 threads); none
+    // when the first is below 2 x fcut (files below ~0.5 GiB), for
     // SHA-256, or without the host tail.  At 1 GiB and 12 threads the host
     // takes 2,985 chunks against 6,060 without the shares, and the call
     // reads 0.87-0.90 x dsx_cut_fd against 0.78-0.84.
@@ -817,7 +822,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #if DSX_DIAG
       if (const char* v = getenv("DSX_FEED_CUT_END")) fcut_end = std::max<uint64_t>(4096, atol(v));
 #endif
-      mids = plan_shares(len, p->max, fcut_end);
+      mids = plan_shares(len, p->max, fcut);
       if (mids.empty()) fcut_end = fcut;
     }
     std::vector<Ev> mid_ev(mids.size());
@@ -1157,7 +1162,7 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   std::vector<IdShare> shares;
   uint64_t end_cut = early_cut;
   if (tail_on && nwin == 1 && c->index_host_tail < 0) {
-    for (const Mid& m : plan_shares(L, maxc, early_cut * 3 / 4)) {
+    for (const Mid& m : plan_shares(L, maxc, early_cut)) {
       const uint64_t landed = std::min(L, (m.at + piece - 1) / piece * piece);
       if (landed >= L) break;
       uint64_t i1 = shares.empty() ? 0 : shares.back().i1;

@@ -136,7 +136,7 @@ def test_index_host_threads(tmp_path, monkeypatch, threads):
             assert n_host == int(np.sum(lens > 131072))
 
 
-@pytest.mark.parametrize("mib,cut1", [(320, 61440), (640, 126976)])
+@pytest.mark.parametrize("mib,cut1", [(320, 81920), (640, 163840)])
 def test_index_host_tail_gpu_shares(tmp_path, monkeypatch, mib, cut1):
     """One window large enough for the GPU's shares during the read (at 1/2,
     3/4, ... of the window, a digest on the digest stream of the chunks
@@ -145,9 +145,10 @@ def test_index_host_tail_gpu_shares(tmp_path, monkeypatch, mib, cut1):
     the usual cut): every ID is hashlib's, and the host took between the
     chunks above the first cut and those above the usual cut.  32 host
     threads -> 28 feeders, cut 28 KiB.  The first cut is the read time after
-    1/2 over the GPU's 58 ns per byte, rounded down to 4 KiB: 320 MiB / 45
-    B/ns -> 61440 (one point: 3/4's would be below 1.5 x 28 KiB); 640 MiB ->
-    126976 (two points)."""
+    1/2 over the shares' 45 ns per byte, rounded down to 4 KiB: 320 MiB / 45
+    B/ns -> 81920 (one point: 3/4's would be below 1.5 x 28 KiB); 640 MiB ->
+    163840 (two points).  Then VerifyIndex of the same list, whose shares take
+    host-known chunk ranges."""
     import concurrent.futures as cf
 
     import desync_amd
