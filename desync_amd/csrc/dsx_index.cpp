@@ -815,10 +815,12 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #endif
     std::vector<Mid> mids;
     if (tail_on && nwin == 1 && c->index_host_tail < 0) {
-      // with the shares the host has fewer bytes: 3/4 of the usual cut
-      // after the last point (64 -> 48 KiB at 12 threads; profiles/r06af,
-      // r06ag: 0.882 / 0.898 x dsx_cut_fd against 0.874 / 0.894)
-      fcut_end = std::max<uint64_t>(kFeedCutBase, (fcut * 3 / 4) & ~4095ull);
+      // with the shares the host has fewer bytes: 11/16 of the usual cut
+      // after the last point (64 -> 44 KiB at 12 threads; 3/4: profiles/r06af,
+      // r06ag, 0.882 / 0.898 x dsx_cut_fd against 0.874 / 0.894 at 64; 44
+      // against 48 / 40 / 36 KiB, r06aq: the call's end 1.88 ms after the last
+      // stitch against 2.04 / 1.89 / 2.07)
+      fcut_end = std::max<uint64_t>(kFeedCutBase, (fcut * 11 / 16) & ~4095ull);
 #if DSX_DIAG
       if (const char* v = getenv("DSX_FEED_CUT_END")) fcut_end = std::max<uint64_t>(4096, atol(v));
 #endif
