@@ -44,14 +44,23 @@ using FillFn = int (*)(void* ud, uint8_t* dst, uint64_t off, uint64_t n);
 // Reads pieces [k*piece, (k+1)*piece) of the source into slot k % K on
 // reader threads, ahead of the consumer, never more than K pieces ahead; from
 // fine_from on (a multiple of piece) the pieces are `fine` bytes.
+// Pieces [0, len): `piece` bytes each up to fine_from (a multiple of piece),
+// `fine` bytes from there on (none when fine_from >= len).
+struct PieceMap {
+  uint64_t len, piece, fine_from, fine, kf, np;
+  PieceMap(uint64_t n, uint64_t pc, uint64_t ff = UINT64_MAX, uint64_t fn = 0)
+      : len(n), piece(pc), fine_from(fn && ff < n ? ff : UINT64_MAX), fine(fn ? fn : pc),
+        kf(fine_from < n ? fine_from / pc : (n + pc - 1) / pc),
+        np(kf + (fine_from < n ? (n - fine_from + fine - 1) / fine : 0)) {}
+  uint64_t off(uint64_t k) const { return k < kf ? k * piece : fine_from + (k - kf) * fine; }
+  uint64_t size(uint64_t k) const { return std::min(k < kf ? piece : fine, len - off(k)); }
+};
+
 class Prefetcher {
  public:
   Prefetcher(FillFn fill, void* ud, uint64_t len, uint64_t piece, uint8_t* const* slots, int nslots,
              int nthreads, uint64_t fine_from = UINT64_MAX, uint64_t fine = 0)
-      : fill_(fill), ud_(ud), len_(len), piece_(piece),
-        fine_from_(fine && fine_from < len ? fine_from : UINT64_MAX), fine_(fine ? fine : piece),
-        kf_(fine_from_ < len ? fine_from_ / piece : (len + piece - 1) / piece),
-        np_(kf_ + (fine_from_ < len ? (len - fine_from_ + fine_ - 1) / fine_ : 0)),
+      : fill_(fill), ud_(ud), map_(len, piece, fine_from, fine), np_(map_.np),
         slots_(slots, slots + nslots), have_(nslots, -1), allow_(nslots), rc_(nslots, 0) {
     for (int s = 0; s < nslots; ++s) allow_[s] = s;
     const int nt = std::max(1, std::min<int>(nthreads, (int)std::min<uint64_t>(np_, 64)));
@@ -64,7 +73,7 @@ class Prefetcher {
     std::unique_lock<std::mutex> lk(m_);
     cv_.wait(lk, [&] { return have_[s] == (int64_t)k; });
     *p = slots_[s];
-    *n = plen(k);
+    *n = map_.size(k);
     return rc_[s];
   }
   // the slot holding piece k may be refilled (its H2D copy has landed)
@@ -99,7 +108,7 @@ class Prefetcher {
         cv_.wait(lk, [&] { return stop_ || allow_[s] == (int64_t)k; });
         if (stop_) return;
       }
-      const int rc = fill_(ud_, slots_[s], poff(k), plen(k));
+      const int rc = fill_(ud_, slots_[s], map_.off(k), map_.size(k));
       {
         std::lock_guard<std::mutex> lk(m_);
         rc_[s] = rc;
@@ -108,14 +117,10 @@ class Prefetcher {
       cv_.notify_all();
     }
   }
-  uint64_t poff(uint64_t k) const { return k < kf_ ? k * piece_ : fine_from_ + (k - kf_) * fine_; }
-  uint64_t plen(uint64_t k) const {
-    const uint64_t o = poff(k);
-    return std::min(k < kf_ ? piece_ : fine_, len_ - o);
-  }
   FillFn fill_;
   void* ud_;
-  uint64_t len_, piece_, fine_from_, fine_, kf_, np_;
+  PieceMap map_;
+  uint64_t np_;
   std::vector<uint8_t*> slots_;
   std::vector<int64_t> have_, allow_;
   std::vector<int> rc_;
@@ -664,11 +669,49 @@ int feed_threads(const dsx_ctx* c) {
 #endif
   return t;
 }
-uint64_t feed_cut(const dsx_ctx* c, int threads) {
-  if (c->index_host_tail > 0) return (uint64_t)c->index_host_tail;  // forced (tests, A/B)
+uint64_t feed_cut_for(int64_t host_tail, int threads) {
+  if (host_tail > 0) return (uint64_t)host_tail;  // forced (tests, A/B)
   const uint64_t cut = kFeedCutBase * (uint64_t)kFeedThreadsBase / (uint64_t)std::max(1, threads);
   return std::min<uint64_t>(128ull << 10, std::max<uint64_t>(kFeedCutBase, (cut + 2047) & ~4095ull));
 }
+uint64_t feed_cut(const dsx_ctx* c, int threads) { return feed_cut_for(c->index_host_tail, threads); }
+
+// run_index's geometry: pieces (pinned slots) tile the windows exactly; a
+// window keeps `pre` bytes of its predecessor in front (>= max + 64, line
+// aligned).  The file's last kFineTail bytes (in its last window) are read,
+// copied and scanned in pieces of piece / kFineDiv when the tail feeder runs
+// (`feeds`): it then sees the long chunks of the call's last piece, the
+// host's last batch, a few MB sooner.  (Smaller pieces throughout slow the
+// read: 8 MiB slots, 28 against 45 GiB/s for dsx_cut_fd, profiles/r06ad.)
+struct IndexGeom {
+  uint64_t pre, piece, W, nwin, fine, fine_from = UINT64_MAX;
+  IndexGeom(uint64_t len, uint64_t max_chunk, uint64_t slot, uint64_t window, bool feeds) {
+    pre = (max_chunk + 64 + kLine - 1) / kLine * kLine;
+    piece = std::min<uint64_t>(slot, std::max<uint64_t>(len, 4096));
+    piece = (piece + 4095) & ~4095ull;
+    W = std::max<uint64_t>(window, 2 * pre);
+    W = (W + piece - 1) / piece * piece;
+    if (W >= len) W = (len + piece - 1) / piece * piece;  // one window
+    nwin = (len + W - 1) / W;
+    uint64_t fine_tail = kFineTail, fine_div = kFineDiv;
+#if DSX_DIAG
+    if (const char* v = getenv("DSX_FINE_TAIL")) fine_tail = (uint64_t)atol(v);
+    if (const char* v = getenv("DSX_FINE_DIV")) fine_div = std::max<uint64_t>(1, atol(v));
+#endif
+    fine = std::max<uint64_t>(4096, (piece / fine_div) & ~4095ull);
+    if (feeds && fine_tail && fine < piece) {
+      const uint64_t last_ws = (nwin - 1) * W;
+      fine_from = std::max(last_ws, (len - std::min(len, fine_tail)) / piece * piece);
+    }
+  }
+};
+
+// With the GPU's shares the host has fewer bytes: after the last point the
+// feeder takes 11/16 of its usual cut (64 -> 44 KiB at 12 threads; 3/4:
+// profiles/r06af, r06ag, 0.882 / 0.898 x dsx_cut_fd against 0.874 / 0.894 at
+// 64; 44 against 48 / 40 / 36 KiB, r06aq: the call's end 1.88 ms after the
+// last stitch against 2.04 / 1.89 / 2.07).
+uint64_t share_end_cut(uint64_t fcut) { return std::max<uint64_t>(kFeedCutBase, (fcut * 11 / 16) & ~4095ull); }
 
 int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn fill, void* ud,
               uint64_t* out_ends, uint8_t* out_ids, uint64_t cap, uint64_t* n_out,
@@ -681,34 +724,12 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
   c->stats.host_tail_chunks = 0;
   if (len == 0) return DSX_OK;  // empty file: no chunks (TestChunkerEmptyFile)
   const uint64_t need = len / p->min + 2;
-  // geometry: pieces (pinned slots) tile the windows exactly; a window keeps
-  // `pre` bytes of its predecessor in front (>= max + 64, line aligned)
-  const uint64_t pre = (p->max + 64 + kLine - 1) / kLine * kLine;
-  uint64_t piece = std::min<uint64_t>(c->index_slot, std::max<uint64_t>(len, 4096));
-  piece = (piece + 4095) & ~4095ull;
-  uint64_t W = std::max<uint64_t>(c->index_window, 2 * pre);
-  W = (W + piece - 1) / piece * piece;
-  if (W >= len) W = (len + piece - 1) / piece * piece;  // one window
-  const uint64_t nwin = (len + W - 1) / W;
-  const uint64_t scan_step = std::max<uint64_t>(piece, kScanStep / piece * piece);
-  // The file's last kFineTail bytes (in its last window) are read, copied and
-  // scanned in pieces of piece / kFineDiv: the tail feeder then sees the long
-  // chunks of the call's last piece, the host's last batch, a few MB sooner.
-  // (Smaller pieces throughout slow the read: 8 MiB slots, 28 against 45
-  // GiB/s for dsx_cut_fd, profiles/r06ad.)
-  uint64_t fine_tail = kFineTail, fine_div = kFineDiv;
-#if DSX_DIAG
-  if (const char* v = getenv("DSX_FINE_TAIL")) fine_tail = (uint64_t)atol(v);
-  if (const char* v = getenv("DSX_FINE_DIV")) fine_div = std::max<uint64_t>(1, atol(v));
-#endif
-  const uint64_t fine = std::max<uint64_t>(4096, (piece / fine_div) & ~4095ull);
-  uint64_t fine_from = UINT64_MAX;
   const bool feeds = algo == DSX_DIGEST_SHA512_256 && out_ids &&
                      (c->index_host_tail > 0 || (c->index_host_tail < 0 && host_sha_vec()));
-  if (feeds && fine_tail && fine < piece) {  // (only the tail feeder gains from them)
-    const uint64_t last_ws = (nwin - 1) * W;
-    fine_from = std::max(last_ws, (len - std::min(len, fine_tail)) / piece * piece);
-  }
+  const IndexGeom g(len, p->max, c->index_slot, c->index_window, feeds);
+  const uint64_t pre = g.pre, piece = g.piece, W = g.W, nwin = g.nwin;
+  const uint64_t fine = g.fine, fine_from = g.fine_from;
+  const uint64_t scan_step = std::max<uint64_t>(piece, kScanStep / piece * piece);
   rc = index_setup(c, piece);
   if (rc) return rc;
   HIPCHK(c, grow(c, c->idx_win[0], pre + W));
@@ -815,12 +836,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #endif
     std::vector<Mid> mids;
     if (tail_on && nwin == 1 && c->index_host_tail < 0) {
-      // with the shares the host has fewer bytes: 11/16 of the usual cut
-      // after the last point (64 -> 44 KiB at 12 threads; 3/4: profiles/r06af,
-      // r06ag, 0.882 / 0.898 x dsx_cut_fd against 0.874 / 0.894 at 64; 44
-      // against 48 / 40 / 36 KiB, r06aq: the call's end 1.88 ms after the last
-      // stitch against 2.04 / 1.89 / 2.07)
-      fcut_end = std::max<uint64_t>(kFeedCutBase, (fcut * 11 / 16) & ~4095ull);
+      fcut_end = share_end_cut(fcut);
 #if DSX_DIAG
       if (const char* v = getenv("DSX_FEED_CUT_END")) fcut_end = std::max<uint64_t>(4096, atol(v));
 #endif
@@ -1338,6 +1354,36 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
 }
 
 }  // namespace
+
+#if DSX_DIAG
+// The plan a one-window dsx_index_* call of `len` bytes makes with the default
+// host tail (-1, AVX-512) at `threads` feeder threads: the feeder's cut, the
+// cut after the GPU's last share, and the shares {at, cut} (returns their
+// count, at most cap); and the pieces it reads (off, size), for tests on the
+// CPU (tests/test_host_logic.py).
+extern "C" int dsx_diag_index_plan(uint64_t len, uint64_t max_chunk, int threads, uint64_t* fcut,
+                                   uint64_t* fcut_end, uint64_t* at, uint64_t* cut, int cap) {
+  *fcut = feed_cut_for(-1, threads);
+  const std::vector<Mid> m = plan_shares(len, max_chunk, *fcut);
+  *fcut_end = m.empty() ? *fcut : share_end_cut(*fcut);
+  const int n = (int)std::min<size_t>(m.size(), (size_t)std::max(0, cap));
+  for (int i = 0; i < n; ++i) {
+    at[i] = m[i].at;
+    cut[i] = m[i].cut;
+  }
+  return (int)m.size();
+}
+extern "C" uint64_t dsx_diag_index_pieces(uint64_t len, uint64_t max_chunk, uint64_t slot, uint64_t window,
+                                          int feeds, uint64_t* off, uint64_t* size, uint64_t cap) {
+  const IndexGeom g(len, max_chunk, slot, window, feeds != 0);
+  const PieceMap pm(len, g.piece, g.fine_from, g.fine);
+  for (uint64_t k = 0; k < pm.np && k < cap; ++k) {
+    off[k] = pm.off(k);
+    size[k] = pm.size(k);
+  }
+  return pm.np;
+}
+#endif
 
 void index_release(dsx_ctx* c) {
   c->idx_dg_stream = nullptr;  // (idx_side[0])

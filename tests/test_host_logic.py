@@ -405,3 +405,79 @@ def test_smu_summary_window():
     assert abs(out["j_per_gib"] - 1400 * 1.5 / 3) < 1
     assert abs(out["j_per_gib_above_idle"] - 1150 * 1.5 / 3) < 1
     assert abs(out["res_ppt"] - 350 / 750) < 0.01  # (PPT active over samples 200..599)
+
+
+def _diag_lib():
+    import ctypes
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "desync_amd",
+                        "libdsx_diag.so")
+    if not os.path.exists(path):
+        pytest.skip("libdsx_diag.so not built (make -C desync_amd/csrc diag)")
+    lib = ctypes.CDLL(path)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    lib.dsx_diag_index_plan.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, u64p, u64p,
+                                        u64p, u64p, ctypes.c_int]
+    lib.dsx_diag_index_plan.restype = ctypes.c_int
+    lib.dsx_diag_index_pieces.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_int, u64p, u64p, ctypes.c_uint64]
+    lib.dsx_diag_index_pieces.restype = ctypes.c_uint64
+    return lib
+
+
+@pytest.mark.parametrize("length,threads,fcut,fcut_end,shares", [
+    # 1 GiB at the box's 12 feeder threads: two shares (the first half wholly
+    # on the GPU), 44 KiB after them
+    (1 << 30, 12, 65536, 45056, [(1 << 29, 262144), (3 << 28, 131072)]),
+    # tests/test_gpu_index.py::test_index_host_tail_gpu_shares' cases
+    ((320 << 20) + 4321, 28, 28672, 28672, [(((320 << 20) + 4321) // 2, 81920)]),
+    ((640 << 20) + 4321, 28, 28672, 28672, [(((640 << 20) + 4321) // 2, 163840),
+                                            (3 * ((640 << 20) + 4321) // 4, 81920)]),
+    # too short for a share at 1/2; one thread: the cut clamps at 128 KiB
+    (64 << 20, 12, 65536, 65536, []),
+    (1 << 30, 1, 131072, 90112, [(1 << 29, 262144)]),
+])
+def test_index_share_plan(length, threads, fcut, fcut_end, shares):
+    """The one-window IndexFromFile plan (dsx_index.cpp plan_shares,
+    feed_cut_for, share_end_cut): the feeder's cut from its threads, the GPU's
+    shares at 1/2, 3/4, ... with cut = the read time left / 45 ns per byte,
+    stopping below 1.5 x the feeder's cut, and 11/16 of it after them."""
+    import ctypes
+    lib = _diag_lib()
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    at, cut = (ctypes.c_uint64 * 8)(), (ctypes.c_uint64 * 8)()
+    n = lib.dsx_diag_index_plan(length, 256 << 10, threads, ctypes.byref(a), ctypes.byref(b), at, cut, 8)
+    assert (a.value, b.value) == (fcut, fcut_end)
+    got = [(at[i], cut[i]) for i in range(n)]
+    assert [c for _, c in got] == [c for _, c in shares]
+    assert all(abs(x - y) <= 1 for (x, _), (y, _) in zip(got, shares))
+
+
+def test_index_piece_map():
+    """The pieces run_index reads (IndexGeom + PieceMap): they tile the file;
+    32 MiB slots, and with the tail feeder the last 32 MiB of the last window
+    in 8 MiB pieces; windows stay whole multiples of the slot."""
+    import ctypes
+    import random
+    lib = _diag_lib()
+    slot, window = 32 << 20, 1 << 30
+    rnd = random.Random(5)
+    cases = [1, 4095, 4096, 8 << 20, (32 << 20) + 1, 1 << 30, (1 << 30) + 12345, (3 << 30) - 7]
+    cases += [rnd.randrange(1, 5 << 30) for _ in range(40)]
+    for length in cases:
+        for feeds in (0, 1):
+            cap = 4096
+            off, size = (ctypes.c_uint64 * cap)(), (ctypes.c_uint64 * cap)()
+            n = lib.dsx_diag_index_pieces(length, 256 << 10, slot, window, feeds, off, size, cap)
+            assert 0 < n <= cap
+            pos = 0
+            for k in range(n):
+                assert off[k] == pos and 0 < size[k] <= slot, (length, feeds, k)
+                pos += size[k]
+            assert pos == length
+            piece = min(slot, max(length, 4096) + 4095 & ~4095)
+            fine = [k for k in range(n) if size[k] < piece and off[k] + size[k] < length]
+            if not feeds or piece <= 4 * 4096:
+                assert not fine, (length, feeds)
+            else:
+                # the small pieces are the file's last 32 MiB (rounded down to
+                # a slot), inside its last window
+                assert all(off[k] >= length - (32 << 20) - piece for k in fine), (length, feeds)
