@@ -7,18 +7,27 @@
 // digest.go:11-29); GetFileSize (ioctl_linux.go:63-84) sizes regular files
 // and block devices.
 //
-// Pipeline (one context, two HIP streams, reader threads):
-//   reader threads  pread/memcpy 32 MiB pieces into a ring of pinned slots;
-//   copy_stream     H2D of each piece into the current HBM window;
+// Pipeline (one context, reader threads, HIP streams in three priority pools
+// so that none shares an HSA queue with another -- tools/queue_probe.hip):
+//   reader threads  pread/memcpy 32 MiB pieces into a ring of pinned slots
+//                   (the file's last 32 MiB in 8 MiB pieces);
+//   copy_stream     H2D of each piece into the current HBM window (high);
 //   stream          scan + stitch (dsx_scan.hip, dsx_stitch.hip) every
 //                   32 MiB, the chain state carried on the device; at the
 //                   end of a window a snapshot of {total cuts, carried cut}
-//                   and digest_kernel over the chunks the window finished.
+//                   (high);
+//   idx_side[0..3]  the windows' digests (idx_side[0] = idx_dg_stream) and,
+//                   in a one-window call, the GPU's shares of the window
+//                   during the read (low);
+//   tail feeder     the last window's long chunks hashed on the host as the
+//                   stitches confirm them (its copy stream at the default
+//                   priority), the GPU's last digest skipping them.
 // Two windows alternate, so the digest of window w overlaps the H2D and scan
 // of window w+1.  A window starts with the last max + 128 bytes of the
 // previous one: the carried cut lies in (P - max, P] (dsx_stitch.hip), so the
 // unfinished chunk and the scan's 48-byte warm-up are always in HBM.  No host
-// round trip happens until the end of the file.
+// round trip happens until the end of the file but the feeder's (DESIGN.md
+// 5.1).
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
