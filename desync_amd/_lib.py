@@ -159,7 +159,7 @@ DIAG_ENV = {"DSX_SCAN_VARIANT": "0", "DSX_SCAN_CFG": "0", "DSX_FUSE": "0", "DSX_
             "DSX_STREAM_BATCH": None, "DSX_NOOP_BEFORE_SCAN": None, "DSX_WALK_WGS": "2",
             "DSX_WALK_NT": "576", "DSX_TAIL_LOG": None, "DSX_FEED_THREADS": None, "DSX_FEED_MULTI": None,
             "DSX_FEED_MID": None, "DSX_SIDE_PRIO": "1",
-            "DSX_FEED_CUT_END": None, "DSX_SHARE_NS": "58", "DSX_SHARE_PC": "1", "DSX_SHARE_SLACK": "0", "DSX_CTX_PRIO": "1", "DSX_FEED_EXTRA": None, "DSX_FINE_TAIL": "33554432", "DSX_FINE_DIV": "4"}
+            "DSX_FEED_CUT_END": None, "DSX_SHARE_NS": "58", "DSX_SHARE_PC": "1", "DSX_SHARE_SLACK": "0", "DSX_CTX_PRIO": "1", "DSX_FEED_EXTRA": None, "DSX_SHARE_MULTI": "1", "DSX_FINE_TAIL": "33554432", "DSX_FINE_DIV": "4"}
 
 
 def lib():

@@ -843,13 +843,23 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
 #if DSX_DIAG
     if (const char* v = getenv("DSX_SHARE_PC")) share_pc = atoi(v);
 #endif
+    // (several windows: the last one's shares, on side streams 1.. -- side
+    // stream 0 carries the previous window's digest meanwhile)
+    bool share_multi = true;
+#if DSX_DIAG
+    if (const char* v = getenv("DSX_SHARE_MULTI")) share_multi = atoi(v) != 0;
+#endif
+    const uint64_t last_ws = (nwin - 1) * W, last_wl = len - last_ws;
+    const size_t side0 = nwin > 1 ? 1 : 0;  // the first side stream of the shares
     std::vector<Mid> mids;
-    if (tail_on && nwin == 1 && c->index_host_tail < 0) {
+    if (tail_on && (nwin == 1 || share_multi) && c->index_host_tail < 0) {
       fcut_end = share_end_cut(fcut);
 #if DSX_DIAG
       if (const char* v = getenv("DSX_FEED_CUT_END")) fcut_end = std::max<uint64_t>(4096, atol(v));
 #endif
-      mids = plan_shares(len, p->max, fcut);
+      mids = plan_shares(last_wl, p->max, fcut);
+      if (mids.size() > (size_t)dsx_ctx::kIdxSide - side0) mids.resize(dsx_ctx::kIdxSide - side0);
+      for (Mid& m : mids) m.at += last_ws;
       if (mids.empty()) fcut_end = fcut;
     }
     std::vector<Ev> mid_ev(mids.size());
@@ -912,23 +922,24 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
             e = hipEventRecord(mid_ev[m].e, c->stream);
             if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: record"));
             DigestArgs dm{};
-            dm.blob = buf + pre;
-            dm.base_off = 0;
-            dm.len = end;
+            dm.blob = w == 0 ? buf + pre : buf;
+            dm.base_off = w == 0 ? 0 : ws - pre;
+            dm.len = w == 0 ? end : pre + (end - ws);
             dm.ends = c->out.p;
             dm.ids = c->dg_ids.p;
-            dm.range_lo = m ? mid_snap(m - 1) : c->idx_snap.p;
+            dm.range_lo = m ? mid_snap(m - 1) : c->idx_snap.p + 2 * w;
             dm.range_hi = mid_snap(m);
             dm.skip_above = mids[m].cut >= p->max ? 0 : mids[m].cut;
-            // (on side stream m after this stitch: the shares run side by side)
-            hipStream_t ss = c->idx_side[m];
+            // (on its own side stream after this stitch: the shares run side by side)
+            hipStream_t ss = c->idx_side[side0 + m];
             e = hipStreamWaitEvent(ss, mid_ev[m].e, 0);
             if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "index: wait"));
             // (digest_pc_kernel: its chain ran ~45 ns/B during the read,
             // digest_kernel's ~85, profiles/r06aa, r06ab)
-            const uint64_t from = m ? mids[m - 1].at : 0;
+            const uint64_t from = m ? mids[m - 1].at : ws;
             rc = launch_digest(c, dm, (end - from + 2 * p->max) / p->min + 2, algo, ss,
-                               c->idx_side_q.p + 32 * m, false, (uint32_t)(c->ncu * 3 / 4), share_pc);
+                               c->idx_side_q.p + 32 * (side0 + m), false, (uint32_t)(c->ncu * 3 / 4),
+                               share_pc);
             if (rc) return drain(c, pf, rc);
             feed->add_boundary(mid_ev[m].e, mid_snap(m), m + 1 < mids.size() ? mids[m + 1].cut : fcut_end);
 #if DSX_DIAG
@@ -1013,7 +1024,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
             (void)hipStreamSynchronize(c->stream);
             const double gms =
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
-            for (size_t m = 0; m < mids_done; ++m) (void)hipStreamSynchronize(c->idx_side[m]);
+            for (size_t m = 0; m < mids_done; ++m) (void)hipStreamSynchronize(c->idx_side[side0 + m]);
             const double sms =
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
             fprintf(stderr, "feed: chunks %lu host %zu (cut %lu) host done %.2f ms, GPU done %.2f ms, shares done %.2f ms\n",
@@ -1056,7 +1067,7 @@ int run_index(dsx_ctx* c, const dsx_params_t* p, int algo, uint64_t len, FillFn 
     rc = read_state(c, &st);  // (the stitches)
     HIPCHK(c, hipStreamSynchronize(c->copy_stream));
     HIPCHK(c, hipStreamSynchronize(c->idx_dg_stream));  // (the digests)
-    for (size_t m = 0; m < mids_done; ++m) HIPCHK(c, hipStreamSynchronize(c->idx_side[m]));
+    for (size_t m = 0; m < mids_done; ++m) HIPCHK(c, hipStreamSynchronize(c->idx_side[side0 + m]));
     if (rc) return rc;
     if (st.err & kErrDense) {  // rare: a lane overflowed its candidate slots
       c->stats.dense_fallbacks++;

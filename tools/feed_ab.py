@@ -86,9 +86,11 @@ def main():
                     # `_tN`: the last N MiB in finer pieces, DSX_FINE_TAIL, 0 off;
                     # `_dN`: of slot / N bytes, DSX_FINE_DIV;
                     # `_sN`: the shares may end N us after the read, DSX_SHARE_SLACK;
-                    # `_xN`: N hashers join once the reads are done, DSX_FEED_EXTRA)
+                    # `_xN`: N hashers join once the reads are done, DSX_FEED_EXTRA;
+                    # `_u0`: no shares in the last of several windows, DSX_SHARE_MULTI=0)
                     for v in ("DSX_FEED_MID", "DSX_FEED_CUT_END", "DSX_SHARE_NS", "DSX_SHARE_PC",
-                              "DSX_FINE_TAIL", "DSX_FINE_DIV", "DSX_SHARE_SLACK", "DSX_FEED_EXTRA"):
+                              "DSX_FINE_TAIL", "DSX_FINE_DIV", "DSX_SHARE_SLACK", "DSX_FEED_EXTRA",
+                              "DSX_SHARE_MULTI"):
                         os.environ.pop(v, None)
                     for part in name.split("_")[1:]:
                         if part == "nomid":
@@ -113,6 +115,8 @@ def main():
                             os.environ["DSX_SHARE_PC"] = part[1:]
                         elif part[:1] == "x" and part[1:].isdigit():
                             os.environ["DSX_FEED_EXTRA"] = part[1:]
+                        elif part[:1] == "u" and part[1:].isdigit():
+                            os.environ["DSX_SHARE_MULTI"] = part[1:]
                     if c.startswith("cut"):
                         t0 = time.perf_counter()
                         desync_amd.cut_fd(fdr, MIN, AVG, MAX, ctx=ctxs[key(c)])
