@@ -1199,11 +1199,20 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
   };
   std::vector<IdShare> shares;
   uint64_t end_cut = early_cut;
-  if (tail_on && nwin == 1 && c->index_host_tail < 0) {
-    for (const Mid& m : plan_shares(L, maxc, early_cut)) {
-      const uint64_t landed = std::min(L, (m.at + piece - 1) / piece * piece);
-      if (landed >= L) break;
-      uint64_t i1 = shares.empty() ? 0 : shares.back().i1;
+  // (several windows: the last one's, on side streams 0.., planned over its
+  // length; the windows' digests run on `stream` here)
+  const uint64_t last_ws = (nwin - 1) * W;
+  uint64_t i_last = 0;  // the last window's first chunk (the first ending past last_ws)
+  while (nwin > 1 && i_last < n && ends[i_last] - start <= last_ws) ++i_last;
+  bool share_multi = true;
+#if DSX_DIAG
+  if (const char* v = getenv("DSX_SHARE_MULTI")) share_multi = atoi(v) != 0;
+#endif
+  if (tail_on && (nwin == 1 || share_multi) && c->index_host_tail < 0) {
+    for (const Mid& m : plan_shares(L - last_ws, maxc, early_cut)) {
+      const uint64_t landed = std::min(L, (last_ws + m.at + piece - 1) / piece * piece);
+      if (landed >= L || shares.size() >= (size_t)dsx_ctx::kIdxSide) break;
+      uint64_t i1 = shares.empty() ? i_last : shares.back().i1;
       while (i1 < n && ends[i1] - start <= landed) ++i1;
       shares.push_back({landed, m.cut, i1});
     }
@@ -1212,7 +1221,7 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       // segment's above end_cut
       uint64_t fixed = 0;
       std::vector<uint64_t> last;
-      for (uint64_t i = 0, k = 0; i < n; ++i) {
+      for (uint64_t i = i_last, k = 0; i < n; ++i) {
         while (k < shares.size() && i >= shares[k].i1) ++k;
         const uint64_t ln = ends[i] - (i ? ends[i - 1] : start);
         if (k < shares.size()) {
@@ -1240,12 +1249,12 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
 #endif
     }
   }
-  if (tail_on) {
-    const uint64_t last_ws = (nwin - 1) * W;  // (the last window: chunks ending past it)
+  if (tail_on) {  // (the last window: chunks ending past last_ws)
     for (uint64_t i = 0, k = 0; i < n; ++i) {
       const uint64_t s0 = i ? ends[i - 1] - start : 0, e0 = ends[i] - start;
       while (k < shares.size() && i >= shares[k].i1) ++k;
       const uint64_t cut = k < shares.size() ? shares[k].cut : (shares.empty() ? early_cut : end_cut);
+      if (i < i_last) continue;  // (k counts segments from the last window's first chunk)
       if ((nwin == 1 || e0 > last_ws) && e0 - s0 > cut) early.push_back({i, s0, e0 - s0});
     }
     std::sort(early.begin(), early.end(), [](const TailChunk& a, const TailChunk& b) { return a.len > b.len; });
@@ -1279,15 +1288,15 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
       if (shares_done < shares.size() && off + hn >= shares[shares_done].landed) {
         // share m: its chunks' bytes have landed once this copy has
         const size_t m = shares_done++;
-        const uint64_t a = m ? shares[m - 1].i1 : 0, b = shares[m].i1;
+        const uint64_t a = m ? shares[m - 1].i1 : i_last, b = shares[m].i1;
         if (b > a) {
           hipStream_t ss = c->idx_side[m];
           e = hipStreamWaitEvent(ss, c->idx_copy_ev[k % K], 0);
           if (e != hipSuccess) return drain(c, pf, set_hip_err(c, e, "ids: wait"));
           DigestArgs dm{};
-          dm.blob = buf + pre;
-          dm.base_off = 0;
-          dm.len = shares[m].landed;
+          dm.blob = w == 0 ? buf + pre : buf;
+          dm.base_off = w == 0 ? 0 : ws - pre;
+          dm.len = w == 0 ? shares[m].landed : pre + (shares[m].landed - ws);
           dm.ends = c->dg_ends.p + a;
           dm.first_start = a == 0 ? 0 : ends[a - 1] - start;
           dm.n = b - a;

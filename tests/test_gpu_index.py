@@ -268,13 +268,16 @@ def test_index_host_tail(tmp_path, monkeypatch, tail, window):
 
 def test_index_host_two_gib_windows():
     """1.5 GiB through the default 1 GiB windows (two of them): every cut
-    against oracle.chunk_parallel, every ID against hashlib."""
+    against oracle.chunk_parallel, every ID against hashlib -- also those of
+    VerifyIndex over the same list (the last window's GPU shares in both:
+    snapshot ranges in dsx_index_host, host-known ranges in dsx_ids_host)."""
     import concurrent.futures as cf
 
     import desync_amd
     n = (3 << 29) + 777
     data = o.synth_uniform_c(17, 0, n)
     ends, ids = desync_amd.index_host(data, MIN, AVG, MAX)
+    vids = desync_amd.ids_host(data, 0, ends)
     ref = o.chunk_parallel(data, MIN, AVG, MAX, o.default_threads())
     assert np.array_equal(ends, ref)
     starts = np.concatenate([[0], ref[:-1]]).astype(np.uint64)
@@ -286,6 +289,7 @@ def test_index_host_two_gib_windows():
     with cf.ThreadPoolExecutor(o.default_threads()) as pool:
         want = list(pool.map(h, range(ref.size), chunksize=256))
     assert [bytes(x) for x in ids] == want
+    assert [bytes(x) for x in vids] == want
 
 
 def test_urandom_file(tmp_path):
