@@ -248,6 +248,28 @@ constexpr double kGpuNsPerByte = 58.0;   // digest_pc_kernel, one lane, end of a
 constexpr double kShareNsPerByte = 45.0;  // the same beside the read's scans (37-40, r06an)
 constexpr double kReadBytesPerNs = 45.0;  // page cache -> HBM through the pinned slots (dsx_cut_fd, ~42 GiB/s)
 constexpr double kHostNsPerByte = 0.38;  // one host thread, read + hash (AVX-512)
+
+// This host's SHA-512/256 rate, ns per byte on one thread (8 lanes of 128 KiB
+// hashed once per process, ~0.5 ms), plus the read: the VerifyIndex budget
+// takes the slower of it and kHostNsPerByte, so a slower host gets fewer
+// bytes instead of a call that waits for its early hash.
+double host_ns_per_byte() {
+  static const double v = [] {
+    if (!host_sha_vec()) return 4.0 * kHostNsPerByte;  // (the scalar path)
+    constexpr uint64_t n = 128 << 10;
+    std::vector<uint8_t> buf(8 * n, 0x5a), out(8 * 32);
+    const uint8_t* p[8];
+    uint64_t len[8];
+    uint8_t* o[8];
+    for (int i = 0; i < 8; ++i) p[i] = buf.data() + i * n, len[i] = n, o[i] = out.data() + 32 * i;
+    host_sha512_256_x8(p, len, o);  // (warm)
+    const auto t0 = std::chrono::steady_clock::now();
+    host_sha512_256_x8(p, len, o);
+    const double ns = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+    return 1.15 * ns / (8.0 * (double)n);  // (+15 %: the read through `fill`)
+  }();
+  return std::max(v, kHostNsPerByte);
+}
 constexpr double kTailMinGainNs = 5e5;   // worth a host pass only above this
 constexpr int kTailThreads = 16;
 constexpr size_t kMaxMids = dsx_ctx::kIdxSide;  // GPU shares of a one-window call during its read
@@ -1231,7 +1253,7 @@ int run_ids(dsx_ctx* c, int algo, uint64_t len, FillFn fill, void* ud, uint64_t 
         }
       }
       std::sort(last.begin(), last.end());
-      const double budget = 0.75 * (double)L / kReadBytesPerNs * eth / kHostNsPerByte;  // bytes
+      const double budget = 0.75 * (double)L / kReadBytesPerNs * eth / host_ns_per_byte();  // bytes
       // the lowest cut (4 KiB steps up to early_cut) whose host bytes fit
       uint64_t tail_bytes = 0;
       for (uint64_t x : last) tail_bytes += x;
